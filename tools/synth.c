@@ -1,0 +1,110 @@
+/*
+ * synth.c -- canonical synthetic libsvm / CSV generator (bench + test input).
+ *
+ * Deterministic per row: row r draws from splitmix64 seeded with
+ * mix(seed, r), so any row range can be produced independently (sharded
+ * generation for multi-GPU runs, parallel generation with OpenMP).
+ *
+ *  libsvm row: "<label>( <id>:<value>)*\n", label = 1 random bit, exactly K
+ *    features, ids strictly increasing (first = gap-1, then += gap, gap
+ *    uniform in [1,16]), value = fp32 uniform [0,1) from a 24-bit mantissa,
+ *    printed "%.9g" (round-trips exactly).
+ *  CSV row: C values uniform [-1,1) (24-bit mantissa), "%.9g", ',' separated.
+ */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+static inline uint64_t sm64(uint64_t *x) {
+  uint64_t z = (*x += 0x9E3779B97F4A7C15ULL);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+static inline uint64_t row_state(uint64_t seed, uint64_t r) {
+  uint64_t s = seed * 0xD1B54A32D192ED03ULL ^ (r + 1) * 0x9E3779B97F4A7C15ULL;
+  sm64(&s);
+  return s;
+}
+
+static size_t fmt_libsvm_row(char *o, uint64_t seed, uint64_t r, int K) {
+  uint64_t s = row_state(seed, r);
+  char *p = o;
+  *p++ = (char)('0' + (sm64(&s) & 1));
+  uint64_t id = 0;
+  for (int j = 0; j < K; ++j) {
+    uint64_t x = sm64(&s);
+    uint64_t gap = 1 + (x & 15);
+    id = j == 0 ? gap - 1 : id + gap;
+    float v = (float)(x >> 40) * (1.0f / 16777216.0f);
+    p += sprintf(p, " %llu:%.9g", (unsigned long long)id, (double)v);
+  }
+  *p++ = '\n';
+  return (size_t)(p - o);
+}
+
+static size_t fmt_csv_row(char *o, uint64_t seed, uint64_t r, int C) {
+  uint64_t s = row_state(seed, r);
+  char *p = o;
+  for (int j = 0; j < C; ++j) {
+    uint64_t x = sm64(&s);
+    float v = (float)(x >> 40) * (1.0f / 8388608.0f) - 1.0f;
+    p += sprintf(p, j ? ",%.9g" : "%.9g", (double)v);
+  }
+  *p++ = '\n';
+  return (size_t)(p - o);
+}
+
+/* upper bound on the bytes of `nrows` rows */
+size_t synth_bound(int fmt, uint64_t nrows, int width) {
+  return fmt == 0 ? nrows * (size_t)(2 + width * 26) : nrows * (size_t)(width * 18 + 2);
+}
+
+/* Format rows [row0, row0+nrows) into out (capacity cap); returns bytes, or 0
+ * if cap is too small.  If line_off != NULL it receives nrows+1 line offsets. */
+size_t synth_rows(int fmt, uint64_t row0, uint64_t nrows, int width, uint64_t seed, char *out,
+                  size_t cap, uint64_t *line_off) {
+  const int nblk = 256;
+  uint64_t per = (nrows + nblk - 1) / nblk;
+  size_t *bsz = (size_t *)calloc(nblk, sizeof(size_t));
+  char **bbuf = (char **)calloc(nblk, sizeof(char *));
+  int overflow = 0;
+#pragma omp parallel for schedule(dynamic, 1)
+  for (int b = 0; b < nblk; ++b) {
+    uint64_t r0 = (uint64_t)b * per, r1 = r0 + per < nrows ? r0 + per : nrows;
+    if (r0 >= r1) continue;
+    size_t cap_b = synth_bound(fmt, r1 - r0, width);
+    char *buf = (char *)malloc(cap_b + 64);
+    size_t n = 0;
+    for (uint64_t r = r0; r < r1; ++r) {
+      if (line_off) line_off[r] = n; /* block-relative; fixed below */
+      n += fmt == 0 ? fmt_libsvm_row(buf + n, seed, row0 + r, width)
+                    : fmt_csv_row(buf + n, seed, row0 + r, width);
+    }
+    bbuf[b] = buf;
+    bsz[b] = n;
+  }
+  size_t total = 0;
+  for (int b = 0; b < nblk; ++b) total += bsz[b];
+  if (total > cap) overflow = 1;
+  if (!overflow) {
+    size_t *base = (size_t *)calloc(nblk, sizeof(size_t));
+    for (int b = 1; b < nblk; ++b) base[b] = base[b - 1] + bsz[b - 1];
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int b = 0; b < nblk; ++b) {
+      if (!bsz[b]) continue;
+      memcpy(out + base[b], bbuf[b], bsz[b]);
+      if (line_off) {
+        uint64_t r0 = (uint64_t)b * per, r1 = r0 + per < nrows ? r0 + per : nrows;
+        for (uint64_t r = r0; r < r1; ++r) line_off[r] += base[b];
+      }
+    }
+    if (line_off) line_off[nrows] = total;
+    free(base);
+  }
+  for (int b = 0; b < nblk; ++b) free(bbuf[b]);
+  free(bbuf);
+  free(bsz);
+  return overflow ? 0 : total;
+}
