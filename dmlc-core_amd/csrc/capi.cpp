@@ -1,0 +1,161 @@
+// capi.cpp -- the extern "C" boundary (include/dmlc_amd.h) over the HIP kernels.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+
+#include "dmlc_amd.h"
+#include "dmlc_amd_kernels.h"
+
+namespace {
+
+constexpr uint64_t kDefaultTile = 256ull << 10;  // bytes of text owned per workgroup
+constexpr int kSlots = 7;
+
+uint64_t tile_of(const dmlc_amd_params *p) {
+  return p && p->tile_bytes ? (uint64_t)p->tile_bytes : kDefaultTile;
+}
+
+struct Carve {
+  char *p;
+  size_t left;
+  template <typename T>
+  T *take(size_t n) {
+    size_t bytes = (n * sizeof(T) + 255) & ~size_t(255);
+    if (bytes > left) return nullptr;
+    T *r = reinterpret_cast<T *>(p);
+    p += bytes;
+    left -= bytes;
+    return r;
+  }
+};
+
+// Delimiters that ParseFloat / strtoll can consume, which would make the field
+// structure depend on decoding (csv_parser.h:99-127): handled by the exact
+// per-line path instead of the field-parallel one.
+bool csv_delim_fast(int d, int vtype) {
+  const unsigned c = (unsigned)d & 0xFFu;
+  if (c == ' ' || (c >= '\t' && c <= '\r')) return false;  // whitespace (incl. \v for strtoll)
+  if ((c >= '0' && c <= '9') || ((c | 32u) >= 'a' && (c | 32u) <= 'z')) return false;
+  if (c == '+' || c == '-' || c == '.' || c == '_' || c == '(' || c == ')') return false;
+  if (c == 0) return false;
+  (void)vtype;
+  return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dmlc_amd_abi_version(void) { return DMLC_AMD_ABI_VERSION; }
+
+int dmlc_amd_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+const char *dmlc_amd_error_string(int code) {
+  switch (code) {
+    case DMLC_AMD_OK: return "ok";
+    case DMLC_AMD_ERR_NEG_INDEX: return "Check failed: sign == true";
+    case DMLC_AMD_ERR_NAN_LITERAL: return "Check failed: *p == ')': Invalid NAN literal";
+    case DMLC_AMD_ERR_CSV_DELIM: return "Delimiter is not found in the line";
+    case DMLC_AMD_ERR_CAPACITY: return "output capacity exceeded";
+    case DMLC_AMD_ERR_ARG: return "invalid argument";
+    case DMLC_AMD_ERR_HIP: return "HIP runtime error";
+    default: return "unknown error";
+  }
+}
+
+size_t dmlc_amd_workspace_bytes(uint64_t nbytes, int nchunks, const dmlc_amd_params *prm) {
+  const uint64_t T = tile_of(prm);
+  const uint64_t ntiles = (nbytes + T - 1) / T;
+  const uint64_t nc = nchunks > 0 ? (uint64_t)nchunks : 1;
+  return (size_t)((2 * ntiles * kSlots + nc + nc * 8) * sizeof(uint64_t) + 8 * 256);
+}
+
+int dmlc_amd_parse(const void *d_text, uint64_t nbytes, const uint64_t *d_chunk_starts, int nchunks,
+                   const dmlc_amd_params *prm, const dmlc_amd_csr *out, uint64_t *d_chunk_table,
+                   void *d_workspace, size_t workspace_bytes, dmlc_amd_result *d_result,
+                   void *stream) {
+  if (!prm || !out || !d_result) return DMLC_AMD_ERR_ARG;
+  if (prm->format < DMLC_AMD_LIBSVM || prm->format > DMLC_AMD_LIBFM) return DMLC_AMD_ERR_ARG;
+  if (prm->index_bits != 32 && prm->index_bits != 64) return DMLC_AMD_ERR_ARG;
+  if (prm->value_type < DMLC_AMD_F32 || prm->value_type > DMLC_AMD_I64) return DMLC_AMD_ERR_ARG;
+  if (prm->format != DMLC_AMD_CSV && prm->value_type != DMLC_AMD_F32) return DMLC_AMD_ERR_ARG;
+  if (nbytes && (!d_text || !d_chunk_starts || nchunks < 1)) return DMLC_AMD_ERR_ARG;
+  if (prm->format == DMLC_AMD_CSV && prm->label_column >= 0 &&
+      prm->label_column == prm->weight_column)
+    return DMLC_AMD_ERR_ARG;  // csv_parser.h:59-60
+  if (workspace_bytes < dmlc_amd_workspace_bytes(nbytes, nchunks, prm) || !d_workspace)
+    return DMLC_AMD_ERR_ARG;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const uint64_t T = tile_of(prm);
+  const uint64_t ntiles = (nbytes + T - 1) / T;
+  const int nc = nchunks > 0 ? nchunks : 1;
+  Carve cv{reinterpret_cast<char *>(d_workspace), workspace_bytes};
+  uint64_t *tile_cnt = cv.take<uint64_t>(ntiles * kSlots + 1);
+  uint64_t *tile_base = cv.take<uint64_t>(ntiles * kSlots + 1);
+  uint64_t *chunk_min = cv.take<uint64_t>(nc);
+  uint64_t *chunk_sink = cv.take<uint64_t>((size_t)nc * 8);
+  if (!tile_cnt || !tile_base || !chunk_min || !chunk_sink) return DMLC_AMD_ERR_ARG;
+  uint64_t *res = reinterpret_cast<uint64_t *>(d_result);
+  const bool count_only = (prm->flags & DMLC_AMD_FLAG_COUNT_ONLY) != 0;
+  hipError_t e = hipSuccess;
+  if (prm->format == DMLC_AMD_LIBSVM) {
+    dmlc_amd::LibsvmArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.text = reinterpret_cast<const uint8_t *>(d_text);
+    a.n = nbytes;
+    a.cs = d_chunk_starts;
+    a.nchunk = nchunks;
+    a.tile_bytes = T;
+    a.ntiles = (uint32_t)ntiles;
+    a.wide = prm->index_bits == 64;
+    a.indexing_mode = prm->indexing_mode;
+    a.tile_cnt = tile_cnt;
+    a.tile_base = tile_base;
+    a.offset = out->offset;
+    a.label = reinterpret_cast<float *>(out->label);
+    a.weight = out->weight;
+    a.qid = out->qid;
+    a.index = out->index;
+    a.value = reinterpret_cast<float *>(out->value);
+    for (int i = 0; i < 8; ++i) a.cap[i] = out->cap[i];
+    a.chunk_tab = d_chunk_table ? d_chunk_table : chunk_sink;
+    a.chunk_min = chunk_min;
+    a.err = reinterpret_cast<unsigned long long *>(res + 8);
+    e = dmlc_amd::launch_libsvm(a, res, count_only, s);
+  } else if (prm->format == DMLC_AMD_CSV) {
+    dmlc_amd::CsvArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.text = reinterpret_cast<const uint8_t *>(d_text);
+    a.n = nbytes;
+    a.cs = d_chunk_starts;
+    a.nchunk = nchunks;
+    a.tile_bytes = T;
+    a.ntiles = (uint32_t)ntiles;
+    a.wide = prm->index_bits == 64;
+    a.vtype = prm->value_type;
+    a.label_column = prm->label_column;
+    a.weight_column = prm->weight_column;
+    a.delim = (uint32_t)prm->delimiter & 0xFFu;
+    a.fast_delim = csv_delim_fast(prm->delimiter, prm->value_type);
+    a.tile_cnt = tile_cnt;
+    a.tile_base = tile_base;
+    a.offset = out->offset;
+    a.label = out->label;
+    a.weight = out->weight;
+    a.index = out->index;
+    a.value = out->value;
+    for (int i = 0; i < 8; ++i) a.cap[i] = out->cap[i];
+    a.chunk_tab = d_chunk_table ? d_chunk_table : chunk_sink;
+    a.err = reinterpret_cast<unsigned long long *>(res + 8);
+    e = dmlc_amd::launch_csv(a, res, count_only, s);
+  } else {
+    return DMLC_AMD_ERR_ARG;  // libfm: not built yet
+  }
+  return e == hipSuccess ? DMLC_AMD_OK : DMLC_AMD_ERR_HIP;
+}
+
+}  // extern "C"

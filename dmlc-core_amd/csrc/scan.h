@@ -1,0 +1,48 @@
+// scan.h -- exclusive scan of per-tile counter vectors (single workgroup) and
+// pipeline finalisation.  Included by each kernel translation unit (no RDC).
+#pragma once
+#include "common.h"
+
+namespace dmlc_amd {
+namespace {  // one private copy per kernel translation unit (no RDC)
+
+struct Cnt64 {
+  uint64_t c[8];
+};
+struct Cnt64Add {
+  __device__ Cnt64 operator()(const Cnt64 &a, const Cnt64 &b) const {
+    Cnt64 r;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.c[i] = a.c[i] + b.c[i];
+    return r;
+  }
+};
+
+// tile_base[k] = sum_{j<k} tile_cnt[j]; res[0..C_N) = totals;
+// offset[total_rows] = total index count (the reference's final offset push).
+__global__ void __launch_bounds__(kThreads)
+tile_scan_kernel(const uint64_t *tile_cnt, uint64_t *tile_base, uint32_t ntiles, uint64_t *res,
+                 uint64_t *offset, uint64_t cap_rows) {
+  __shared__ Cnt64 sc[kWaves + 1];
+  const uint32_t per = (ntiles + kThreads - 1) / kThreads;
+  const uint32_t t0 = threadIdx.x * per, t1 = min(t0 + per, ntiles);
+  Cnt64 mine, zero;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) mine.c[i] = zero.c[i] = 0;
+  for (uint32_t k = t0; k < t1; ++k)
+    for (int i = 0; i < C_N; ++i) mine.c[i] += tile_cnt[(uint64_t)k * C_N + i];
+  Cnt64 total;
+  Cnt64 run = block_exclusive(mine, zero, Cnt64Add(), sc, &total);
+  for (uint32_t k = t0; k < t1; ++k)
+    for (int i = 0; i < C_N; ++i) {
+      tile_base[(uint64_t)k * C_N + i] = run.c[i];
+      run.c[i] += tile_cnt[(uint64_t)k * C_N + i];
+    }
+  if (threadIdx.x == 0) {
+    for (int i = 0; i < C_N; ++i) res[i] = total.c[i];
+    if (offset && total.c[C_ROWS] < cap_rows + 1) offset[total.c[C_ROWS]] = total.c[C_INDEX];
+  }
+}
+
+}  // namespace
+}  // namespace dmlc_amd

@@ -1,0 +1,278 @@
+"""Python binding of the MI355X parse path (ctypes over include/dmlc_amd.h).
+
+PyTorch is used only as plumbing: device buffers (torch.cuda tensors) and the
+current HIP stream.  All parsing runs in libdmlc_amd.so's HIP kernels; there is
+no CPU fallback -- importing this module on a machine without the built
+library, or calling parse() without a GPU, raises.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libdmlc_amd.so")
+
+LIBSVM, CSV, LIBFM = 0, 1, 2
+F32, I32, I64 = 0, 1, 2
+ROWS, INDEX, VALUE, WEIGHT, QID, LABEL, FIELD = range(7)
+FLAG_COUNT_ONLY = 1
+ERR_CAPACITY = 16
+_FMT = {"libsvm": LIBSVM, "csv": CSV, "libfm": LIBFM}
+_VT = {"f32": F32, "float32": F32, "i32": I32, "int32": I32, "i64": I64, "int64": I64}
+
+
+class Params(ctypes.Structure):
+    _fields_ = [("format", ctypes.c_int32), ("index_bits", ctypes.c_int32),
+                ("value_type", ctypes.c_int32), ("indexing_mode", ctypes.c_int32),
+                ("label_column", ctypes.c_int32), ("weight_column", ctypes.c_int32),
+                ("delimiter", ctypes.c_int32), ("tile_bytes", ctypes.c_uint32),
+                ("flags", ctypes.c_uint32), ("reserved", ctypes.c_uint32 * 3)]
+
+
+class Csr(ctypes.Structure):
+    _fields_ = [("offset", ctypes.c_void_p), ("label", ctypes.c_void_p), ("weight", ctypes.c_void_p),
+                ("qid", ctypes.c_void_p), ("field", ctypes.c_void_p), ("index", ctypes.c_void_p),
+                ("value", ctypes.c_void_p), ("cap", ctypes.c_uint64 * 8)]
+
+
+_LIB = None
+
+
+def lib():
+    """Load libdmlc_amd.so; raises if it was not built (no silent fallback)."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError("libdmlc_amd.so not built: run `make -C dmlc-core_amd` "
+                               "(or __graft_entry__.build())")
+        L = ctypes.CDLL(LIB_PATH)
+        L.dmlc_amd_workspace_bytes.restype = ctypes.c_size_t
+        L.dmlc_amd_workspace_bytes.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(Params)]
+        L.dmlc_amd_parse.restype = ctypes.c_int
+        L.dmlc_amd_parse.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int,
+                                     ctypes.POINTER(Params), ctypes.POINTER(Csr), ctypes.c_void_p,
+                                     ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p]
+        L.dmlc_amd_error_string.restype = ctypes.c_char_p
+        L.dmlc_amd_error_string.argtypes = [ctypes.c_int]
+        L.dmlc_amd_device_count.restype = ctypes.c_int
+        L.dmlc_amd_abi_version.restype = ctypes.c_int
+        L.dmlc_amd_strtof_batch.restype = ctypes.c_int
+        L.dmlc_amd_strtof_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                            ctypes.c_void_p]
+        _LIB = L
+    return _LIB
+
+
+EXPORTED_SYMBOLS = ("dmlc_amd_parse", "dmlc_amd_workspace_bytes", "dmlc_amd_error_string",
+                    "dmlc_amd_device_count", "dmlc_amd_abi_version", "dmlc_amd_strtof_batch")
+
+
+def make_params(fmt="libsvm", index_bits=32, value_type="f32", indexing_mode=0, label_column=-1,
+                weight_column=-1, delimiter=",", tile_bytes=0, flags=0):
+    p = Params()
+    p.format = _FMT[fmt] if isinstance(fmt, str) else int(fmt)
+    p.index_bits = index_bits
+    p.value_type = _VT[value_type] if isinstance(value_type, str) else int(value_type)
+    p.indexing_mode = indexing_mode
+    p.label_column = label_column
+    p.weight_column = weight_column
+    p.delimiter = ord(delimiter) if isinstance(delimiter, str) else int(delimiter)
+    p.tile_bytes = tile_bytes
+    p.flags = flags
+    return p
+
+
+def _torch():
+    import torch
+    if not torch.cuda.is_available():
+        raise RuntimeError("dmlc_amd: no HIP device visible")
+    return torch
+
+
+def _vdt(torch, vt):
+    return {F32: torch.float32, I32: torch.int32, I64: torch.int64}[vt]
+
+
+class DeviceParser:
+    """One parser configuration bound to the current HIP device.
+
+    parse(text, chunk_starts) takes a device uint8 tensor and a device int64
+    tensor of nchunks+1 chunk boundaries and returns device tensors."""
+
+    def __init__(self, fmt="libsvm", **kw):
+        self.params = make_params(fmt, **kw)
+        self.torch = _torch()
+        self._ws = None
+
+    def _workspace(self, nbytes, nchunks):
+        need = lib().dmlc_amd_workspace_bytes(nbytes, nchunks, ctypes.byref(self.params))
+        if self._ws is None or self._ws.numel() < need:
+            self._ws = self.torch.empty(need, dtype=self.torch.uint8, device="cuda")
+        return self._ws, need
+
+    def _call(self, text, chunk_starts, csr, chunk_table, result, params, stream):
+        torch = self.torch
+        nbytes = int(text.numel())
+        nchunks = int(chunk_starts.numel()) - 1
+        ws, need = self._workspace(nbytes, max(nchunks, 1))
+        s = stream if stream is not None else torch.cuda.current_stream()
+        rc = lib().dmlc_amd_parse(text.data_ptr() if nbytes else None, nbytes,
+                                  chunk_starts.data_ptr() if nbytes else None, nchunks,
+                                  ctypes.byref(params), ctypes.byref(csr),
+                                  chunk_table.data_ptr() if chunk_table is not None else None,
+                                  ws.data_ptr(), ws.numel(), result.data_ptr(), s.cuda_stream)
+        if rc != 0:
+            raise RuntimeError("dmlc_amd_parse: %s" % lib().dmlc_amd_error_string(rc).decode())
+
+    def count(self, text, chunk_starts, stream=None):
+        """Size query: exact per-slot totals (device work, then a host sync)."""
+        torch = self.torch
+        res = torch.zeros(16, dtype=torch.int64, device="cuda")
+        p = Params.from_buffer_copy(self.params)
+        p.flags |= FLAG_COUNT_ONLY
+        self._call(text, chunk_starts, Csr(), None, res, p, stream)
+        return res.cpu().numpy().view(np.uint64)
+
+    def alloc(self, counts):
+        """Allocate exact-size outputs for the given totals."""
+        torch = self.torch
+        wide = self.params.index_bits == 64
+        it = torch.int64 if wide else torch.int32
+        vt = _vdt(torch, self.params.value_type if self.params.format == CSV else F32)
+        c = [int(x) for x in counts]
+        out = {
+            "offset": torch.empty(c[ROWS] + 1, dtype=torch.int64, device="cuda"),
+            "label": torch.empty(max(c[LABEL], 1), dtype=vt, device="cuda"),
+            "weight": torch.empty(max(c[WEIGHT], 1), dtype=torch.float32, device="cuda"),
+            "qid": torch.empty(max(c[QID], 1), dtype=torch.int64, device="cuda"),
+            "field": torch.empty(max(c[FIELD], 1), dtype=it, device="cuda"),
+            "index": torch.empty(max(c[INDEX], 1), dtype=it, device="cuda"),
+            "value": torch.empty(max(c[VALUE], 1), dtype=vt, device="cuda"),
+            "counts": c,
+        }
+        return out
+
+    def csr_of(self, out):
+        csr = Csr()
+        for k in ("offset", "label", "weight", "qid", "field", "index", "value"):
+            setattr(csr, k, out[k].data_ptr())
+        c = out["counts"]
+        caps = [c[ROWS], c[INDEX], c[VALUE], c[WEIGHT], c[QID], c[LABEL], c[FIELD], 0]
+        for i, v in enumerate(caps):
+            csr.cap[i] = v
+        return csr
+
+    def parse_into(self, text, chunk_starts, out, result, chunk_table=None, stream=None):
+        """Launch the full pipeline into preallocated outputs (no host sync)."""
+        self._call(text, chunk_starts, out["_csr"] if "_csr" in out else self.csr_of(out),
+                   chunk_table, result, self.params, stream)
+
+    def parse(self, text, chunk_starts, stream=None):
+        """Count, allocate, parse; returns dict of device tensors + counts/error."""
+        torch = self.torch
+        counts = self.count(text, chunk_starts, stream)
+        out = self.alloc(counts)
+        nchunks = int(chunk_starts.numel()) - 1
+        out["chunk_table"] = torch.zeros(max(nchunks, 1) * 8, dtype=torch.int64, device="cuda")
+        res = torch.zeros(16, dtype=torch.int64, device="cuda")
+        self.parse_into(text, chunk_starts, out, res,
+                        chunk_table=out["chunk_table"] if nchunks > 0 else None, stream=stream)
+        r = res.cpu().numpy().view(np.uint64)
+        out["error"] = int(r[8])
+        out["result_counts"] = [int(x) for x in r[:8]]
+        return out
+
+
+def error_code(err):
+    return int(err) & 0xFFFF
+
+
+def error_pos(err):
+    return int(err) >> 16
+
+
+def to_host(out, index_bits=32, value_type=F32):
+    """Copy parse outputs to numpy with the reference's dtypes."""
+    c = out["counts"]
+    it = np.uint32 if index_bits == 32 else np.uint64
+    vt = {F32: np.float32, I32: np.int32, I64: np.int64}[value_type]
+    h = {
+        "offset": out["offset"][: c[ROWS] + 1].cpu().numpy().view(np.uint64),
+        "label": out["label"][: c[LABEL]].cpu().numpy().view(vt),
+        "weight": out["weight"][: c[WEIGHT]].cpu().numpy().view(np.float32),
+        "qid": out["qid"][: c[QID]].cpu().numpy().view(np.uint64),
+        "field": out["field"][: c[FIELD]].cpu().numpy().view(it),
+        "index": out["index"][: c[INDEX]].cpu().numpy().view(it),
+        "value": out["value"][: c[VALUE]].cpu().numpy().view(vt),
+    }
+    if "chunk_table" in out:
+        h["chunk_table"] = out["chunk_table"].cpu().numpy().view(np.uint64).reshape(-1, 8)
+    return h
+
+
+def parse_bytes(data, chunk_offsets=None, fmt="libsvm", **kw):
+    """Convenience: host bytes -> device -> parse -> host numpy dict."""
+    torch = _torch()
+    raw = data.encode("latin-1") if isinstance(data, str) else bytes(data)
+    if chunk_offsets is None:
+        chunk_offsets = [0, len(raw)] if raw else [0]
+    text = torch.frombuffer(bytearray(raw), dtype=torch.uint8).cuda() if raw else \
+        torch.empty(0, dtype=torch.uint8, device="cuda")
+    cs = torch.tensor(np.asarray(chunk_offsets, dtype=np.int64), device="cuda")
+    p = DeviceParser(fmt, **kw)
+    out = p.parse(text, cs)
+    h = to_host(out, p.params.index_bits,
+                p.params.value_type if p.params.format == CSV else F32)
+    h["error"] = out["error"]
+    h["counts"] = out["counts"]
+    return h
+
+
+def strtof_batch(strings):
+    """Device dmlc::strtof over a list of byte strings -> (f32 values, consumed, nan_err)."""
+    torch = _torch()
+    raws = [s.encode("latin-1") if isinstance(s, str) else bytes(s) for s in strings]
+    offs = np.zeros(len(raws) + 1, dtype=np.int64)
+    offs[1:] = np.cumsum([len(r) for r in raws])
+    blob = b"".join(raws) or b"\0"
+    text = torch.frombuffer(bytearray(blob), dtype=torch.uint8).cuda()
+    d_off = torch.tensor(offs, device="cuda")
+    n = len(raws)
+    out = torch.empty(max(n, 1), dtype=torch.float32, device="cuda")
+    used = torch.empty(max(n, 1), dtype=torch.int32, device="cuda")
+    bad = torch.empty(max(n, 1), dtype=torch.int32, device="cuda")
+    rc = lib().dmlc_amd_strtof_batch(text.data_ptr(), d_off.data_ptr(), n, out.data_ptr(),
+                                     used.data_ptr(), bad.data_ptr(),
+                                     torch.cuda.current_stream().cuda_stream)
+    if rc != 0:
+        raise RuntimeError("dmlc_amd_strtof_batch failed")
+    torch.cuda.synchronize()
+    return out[:n].cpu().numpy(), used[:n].cpu().numpy(), bad[:n].cpu().numpy()
+
+
+def chunk_check(h, fmt, nchunks, total_counts):
+    """Per-chunk consistency CHECKs of the reference, applied to GPU output.
+
+    The reference raises these from RowBlockContainer::GetBlock (row_block.h:
+    174-178) and, for CSV, from ParseBlock itself (csv_parser.h:147-148); libfm
+    adds field == index (libfm_parser.h:127).  Returns the first failing chunk
+    index or -1."""
+    f = _FMT[fmt] if isinstance(fmt, str) else fmt
+    tab = h["chunk_table"][:nchunks].astype(np.int64)
+    ends = np.vstack([tab[1:], np.asarray(total_counts[:8], dtype=np.int64)[None, :]])
+    per = ends - tab
+    for c in range(nchunks):
+        rows, idx, val, w, lab, fld = (per[c, ROWS], per[c, INDEX], per[c, VALUE], per[c, WEIGHT],
+                                       per[c, LABEL], per[c, FIELD])
+        if f == CSV:
+            if lab != 0 and lab != rows:
+                return c
+            if w != 0 and w != rows:
+                return c
+        if f == LIBFM and fld != idx:
+            return c
+        if rows and not (val == 0 or val == idx):
+            return c
+    return -1

@@ -1,0 +1,70 @@
+"""CPU-side checks of the C-ABI library (no GPU needed)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "dmlc-core_amd", "lib", "libdmlc_amd.so")
+
+
+def declared_symbols():
+    syms = set()
+    inc = os.path.join(ROOT, "include")
+    for fn in os.listdir(inc):
+        if fn.endswith(".h"):
+            txt = open(os.path.join(inc, fn)).read()
+            syms |= set(re.findall(r"^\w[\w\s\*]*?\b(dmlc_amd_\w+)\s*\(", txt, re.M))
+    return syms
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not os.path.exists(LIB):
+        import subprocess
+        subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "dmlc-core_amd")])
+    return ctypes.CDLL(LIB)
+
+
+def test_library_loads_and_exports_every_declared_symbol(lib):
+    syms = declared_symbols()
+    assert {"dmlc_amd_parse", "dmlc_amd_workspace_bytes", "dmlc_amd_strtof_batch"} <= syms
+    for s in syms:
+        assert hasattr(lib, s), s
+
+
+def test_python_binding_lists_every_export():
+    import dmlc_amd
+    assert set(dmlc_amd.EXPORTED_SYMBOLS) == declared_symbols()
+
+
+def test_abi_version_and_error_strings(lib):
+    lib.dmlc_amd_abi_version.restype = ctypes.c_int
+    assert lib.dmlc_amd_abi_version() == 1
+    lib.dmlc_amd_error_string.restype = ctypes.c_char_p
+    assert b"sign == true" in lib.dmlc_amd_error_string(1)
+    assert b"NAN" in lib.dmlc_amd_error_string(2)
+
+
+def test_workspace_and_argument_validation(lib):
+    import dmlc_amd
+    p = dmlc_amd.make_params("libsvm")
+    ws = dmlc_amd.lib().dmlc_amd_workspace_bytes(1 << 30, 128, ctypes.byref(p))
+    assert 0 < ws < (1 << 24)
+    # bad index_bits is rejected before any device work
+    bad = dmlc_amd.make_params("libsvm", index_bits=16)
+    csr = dmlc_amd.Csr()
+    rc = dmlc_amd.lib().dmlc_amd_parse(None, 0, None, 0, ctypes.byref(bad), ctypes.byref(csr), None,
+                                      None, 0, None, None)
+    assert rc == 32
+    # csv label_column == weight_column is rejected (csv_parser.h:59-60)
+    c = dmlc_amd.make_params("csv", label_column=1, weight_column=1)
+    rc = dmlc_amd.lib().dmlc_amd_parse(None, 0, None, 0, ctypes.byref(c), ctypes.byref(csr), None,
+                                      None, 0, None, None)
+    assert rc == 32
+
+
+def test_device_count_without_gpu(lib):
+    lib.dmlc_amd_device_count.restype = ctypes.c_int
+    assert lib.dmlc_amd_device_count() >= 0

@@ -1,0 +1,197 @@
+"""GPU parity: the HIP parse path against the reference goldens and the oracle.
+
+All tests run through the C-ABI (libdmlc_amd.so via dmlc_amd.py).  Integer and
+index arrays must be bit-identical; float values bit-identical as well (the
+north star allows 1 ulp, the design targets 0 and the tests demand 0).
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+from golden_util import FIELDS, dec, diff, load_cases, load_floats, load_json, same
+from oracle import pyoracle as po
+from tools import synth
+
+pytestmark = pytest.mark.gpu
+
+FMT_NAME = {po.LIBSVM: "libsvm", po.CSV: "csv", po.LIBFM: "libfm"}
+
+
+@pytest.fixture(scope="module")
+def dm():
+    import dmlc_amd
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    dmlc_amd.lib()
+    return dmlc_amd
+
+
+def gpu_kwargs(params):
+    kw = {}
+    for k, v in params.items():
+        if k == "fmt":
+            continue
+        if k == "value_kind":
+            kw["value_type"] = int(v)
+        elif k == "nthread":
+            continue
+        else:
+            kw[k] = v
+    return kw
+
+
+def gpu_parse(dm, data, chunk_offsets=None, fmt=po.LIBSVM, **kw):
+    name = FMT_NAME[fmt]
+    h = dm.parse_bytes(data, chunk_offsets, fmt=name, **kw)
+    nch = (len(chunk_offsets) - 1) if chunk_offsets is not None else (1 if len(data) else 0)
+    failed = nch > 0 and dm.chunk_check(h, name, nch, h["counts"]) >= 0
+    h["failed"] = bool(h["error"]) or failed
+    return h
+
+
+CASES = [c for c in load_cases() if c["params"]["fmt"] != po.LIBFM]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
+def test_gpu_matches_reference_goldens(dm, case):
+    prm = case["params"]
+    h = gpu_parse(dm, case["data_latin1"], None, prm["fmt"], **gpu_kwargs(prm))
+    if case["status"]:
+        assert h["failed"], "reference raised (%s) but GPU did not" % case["msg"]
+        return
+    assert not h["failed"], (h["error"], h["counts"])
+    exp = {k: dec(v) for k, v in case["expect"].items()}
+    bad = diff(h, exp)
+    assert bad == [], {k: (h[k][:20], exp[k][:20]) for k in bad}
+
+
+def test_gpu_strtof_goldens(dm):
+    strs, bits, used = load_floats()
+    v, n, bad = dm.strtof_batch(strs)
+    got = v.view(np.uint32)
+    mism = np.nonzero((got != bits) | (n != used))[0]
+    assert len(mism) == 0, [(strs[i], hex(bits[i]), hex(got[i]), used[i], n[i]) for i in mism[:10]]
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+@pytest.mark.parametrize("name", ["libsvm_10k_x128", "csv_10k_x256"])
+def test_gpu_synthetic_config1(dm, name):
+    g = load_json("synth_cfg1.json")[name]
+    fmt = po.LIBSVM if g["format"] == "libsvm" else po.CSV
+    text, _ = synth.rows(synth.LIBSVM if fmt == po.LIBSVM else synth.CSV, g["rows"], g["width"],
+                         seed=g["seed"])
+    assert sha(text) == g["input_sha256"]
+    # chunked exactly as the reference's InputSplit would (oracle restatement)
+    chunks = po.split_text([text.tobytes()])
+    offs = np.cumsum([0] + [len(c) for c in chunks])
+    h = gpu_parse(dm, b"".join(chunks), offs, fmt)
+    assert not h["failed"]
+    for k, hv in g["sha256"].items():
+        assert sha(h[k]) == hv, k
+
+
+def _oracle_vs_gpu(dm, data, offs, fmt, **kw):
+    okw = {("value_kind" if k == "value_type" else k): v for k, v in kw.items() if k != "tile_bytes"}
+    o = po.parse_chunks(data, offs, fmt=fmt, **okw)
+    h = gpu_parse(dm, data, offs, fmt, **kw)
+    assert (o["status"] != 0) == h["failed"], (o["msg"], h["error"])
+    if o["status"] == 0:
+        bad = diff(h, o)
+        assert bad == [], bad
+    return h
+
+
+def _random_chunks(rng, data, nmax=8):
+    """Split at random line boundaries like an InputSplit would (after a '\\n' or '\\r')."""
+    nl = [i + 1 for i, b in enumerate(data) if b in (10, 13) and i + 1 < len(data)]
+    k = int(rng.integers(0, min(nmax, len(nl)) + 1)) if nl else 0
+    cuts = sorted(set(rng.choice(nl, size=k, replace=False).tolist())) if k else []
+    return [0] + cuts + [len(data)]
+
+
+@pytest.mark.parametrize("fmt", [po.LIBSVM, po.CSV])
+def test_gpu_multichunk_synthetic_vs_oracle(dm, fmt):
+    rng = np.random.default_rng(7)
+    text, _ = synth.rows(synth.LIBSVM if fmt == po.LIBSVM else synth.CSV, 3000, 37, seed=3)
+    data = text.tobytes()
+    for _ in range(4):
+        _oracle_vs_gpu(dm, data, _random_chunks(rng, data, 12), fmt)
+
+
+@pytest.mark.parametrize("tile", [64, 1000, 4096, 20000])
+def test_gpu_tile_sizes_vs_oracle(dm, tile):
+    """Small tiles put many tile/window boundaries inside lines and heads."""
+    text, _ = synth.rows(synth.LIBSVM, 2000, 50, seed=11)
+    data = text.tobytes()
+    offs = [0, len(data) // 3 + data[len(data) // 3:].index(b"\n") + 1, len(data)]
+    _oracle_vs_gpu(dm, data, offs, po.LIBSVM, tile_bytes=tile)
+    ctext, _ = synth.rows(synth.CSV, 800, 40, seed=12)
+    _oracle_vs_gpu(dm, ctext.tobytes(), [0, len(ctext)], po.CSV, tile_bytes=tile)
+
+
+def test_gpu_long_lines_vs_oracle(dm):
+    """Lines far longer than a window (8 KiB) and than a tile."""
+    rng = np.random.default_rng(5)
+    lines = []
+    for r in range(12):
+        k = int(rng.integers(1, 6000))
+        feats = " ".join("%d:%.9g" % (i * 3, rng.random()) for i in range(k))
+        head = "%d" % (r % 2) + (":0.5" if r % 3 == 0 else "") + (" qid:%d" % r if r % 4 == 0 else "")
+        lines.append(head + " " + feats + (" # tail" if r % 5 == 0 else ""))
+    data = ("\n".join(lines) + "\n").encode()
+    for tile in (0, 4096, 100000):
+        _oracle_vs_gpu(dm, data, [0, len(data)], po.LIBSVM, tile_bytes=tile)
+    csvl = "\n".join(",".join("%.6g" % x for x in rng.random(int(rng.integers(1, 5000))))
+                     for _ in range(8)) + "\n"
+    _oracle_vs_gpu(dm, csvl.encode(), [0, len(csvl)], po.CSV, tile_bytes=4096)
+
+
+def _fuzz_text(rng, fmt):
+    alpha = {po.LIBSVM: list("0123456789") * 6 + list("  ::.-+eE#\tq") + ["qid:", "nan", "inf", "\r"],
+             po.CSV: list("0123456789") * 6 + list(",,,,.-+eE \t") + ["nan", "inf", "0x", "\xef\xbb\xbf"]}[fmt]
+    lines = []
+    for _ in range(int(rng.integers(1, 12))):
+        n = int(rng.integers(0, 60))
+        lines.append("".join(alpha[int(i)] for i in rng.integers(0, len(alpha), n)))
+    t = "\n".join(lines)
+    if rng.random() < 0.5:
+        t += "\n"
+    return t.encode("latin-1")
+
+
+@pytest.mark.parametrize("fmt", [po.LIBSVM, po.CSV])
+def test_gpu_fuzz_vs_oracle(dm, fmt):
+    rng = np.random.default_rng(4242 + fmt)
+    for it in range(300):
+        data = _fuzz_text(rng, fmt)
+        offs = _random_chunks(rng, data, 4) if data else [0]
+        kw = {}
+        if fmt == po.CSV:
+            if rng.random() < 0.3:
+                kw["label_column"] = int(rng.integers(0, 3))
+            if rng.random() < 0.2:
+                kw["value_type"] = int(rng.integers(1, 3))
+            if rng.random() < 0.2:
+                kw["delimiter"] = " "
+        else:
+            if rng.random() < 0.3:
+                kw["indexing_mode"] = int(rng.integers(-1, 2))
+            if rng.random() < 0.2:
+                kw["index_bits"] = 64
+        if rng.random() < 0.3:
+            kw["tile_bytes"] = int(rng.integers(16, 200))
+        try:
+            _oracle_vs_gpu(dm, data, offs, fmt, **kw)
+        except AssertionError as e:
+            raise AssertionError("case %d kw=%s data=%r offs=%s: %s" % (it, kw, data, offs, e))
+
+
+def test_gpu_empty_and_tiny(dm):
+    for fmt in (po.LIBSVM, po.CSV):
+        for d in (b"", b"\n", b"\r\n\r\n", b"1", b"1\n", b"   \n"):
+            offs = [0, len(d)] if d else [0]
+            _oracle_vs_gpu(dm, d, offs, fmt)
