@@ -1,0 +1,55 @@
+// args.h -- argument blocks of the tile kernels (plain C++, shared by the
+// HIP launchers and the test-only CPU emulator).
+#pragma once
+#include <stdint.h>
+
+namespace dmlc_amd {
+
+struct LibsvmArgs {
+  const uint8_t *text;
+  uint64_t n;
+  const uint64_t *cs;  // chunk starts, nchunk + 1 entries, cs[nchunk] == n
+  int nchunk;
+  uint64_t tile_bytes;
+  uint32_t ntiles;
+  int wide;            // IndexType is uint64_t
+  int indexing_mode;
+  uint64_t *tile_cnt;         // [ntiles][C_N], count pass output
+  const uint64_t *tile_base;  // [ntiles][C_N], exclusive scan of tile_cnt
+  uint64_t *offset;
+  float *label;
+  float *weight;
+  uint64_t *qid;
+  void *index;
+  float *value;
+  uint64_t cap[8];
+  uint64_t *chunk_tab;  // [nchunk][C_N] exclusive counts at each chunk start (may be a sink)
+  uint64_t *chunk_min;  // [nchunk] min index per chunk (indexing_mode < 0)
+  unsigned long long *err;
+};
+
+struct CsvArgs {
+  const uint8_t *text;
+  uint64_t n;
+  const uint64_t *cs;
+  int nchunk;
+  uint64_t tile_bytes;
+  uint32_t ntiles;
+  int wide;
+  int vtype;  // 0 f32, 1 i32, 2 i64
+  int label_column, weight_column;
+  uint32_t delim;
+  int fast_delim;  // delimiter cannot be consumed by the field decoder
+  uint64_t *tile_cnt;
+  const uint64_t *tile_base;
+  uint64_t *offset;
+  void *label;  // DType
+  float *weight;
+  void *index;
+  void *value;  // DType
+  uint64_t cap[8];
+  uint64_t *chunk_tab;
+  unsigned long long *err;
+};
+
+}  // namespace dmlc_amd

@@ -1,0 +1,81 @@
+// block.h -- the GPU block policy for the tile bodies: thread id, barrier,
+// block-wide min and exclusive scan over wave64 shuffles + LDS.
+#pragma once
+#include "common.h"
+
+namespace dmlc_amd {
+
+struct DevBlock {
+  // LDS scratch: (kWaves + 1) slots of up to 64 bytes
+  uint64_t *scratch;
+
+  __device__ __forceinline__ int tid() const { return threadIdx.x; }
+  __device__ __forceinline__ void sync() const { __syncthreads(); }
+
+  template <typename T>
+  __device__ __forceinline__ static T shfl_up(T v, int d) {
+    static_assert(sizeof(T) % 4 == 0, "4-byte granular");
+    T o;
+    const int *src = reinterpret_cast<const int *>(&v);
+    int *dst = reinterpret_cast<int *>(&o);
+#pragma unroll
+    for (int k = 0; k < (int)(sizeof(T) / 4); ++k) dst[k] = __shfl_up(src[k], d, kWave);
+    return o;
+  }
+
+  __device__ uint64_t min_u64(uint64_t v) const {
+    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+      const uint64_t o = __shfl_xor(v, d, kWave);
+      v = o < v ? o : v;
+    }
+    if (lane == 0) scratch[wid * 8] = v;
+    __syncthreads();
+    uint64_t r = scratch[0];
+#pragma unroll
+    for (int w = 1; w < kWaves; ++w) r = scratch[w * 8] < r ? scratch[w * 8] : r;
+    __syncthreads();
+    return r;
+  }
+
+  // Exclusive prefix (identity for thread 0) and the block total.
+  template <typename T, typename Op>
+  __device__ T exclusive(T v, T identity, Op op, T *total) const {
+    static_assert(sizeof(T) <= 64, "scan element too large");
+    T *sc = reinterpret_cast<T *>(scratch);
+    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+    T inc = v;
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+      T o = shfl_up(inc, d);
+      if (lane >= d) inc = op(o, inc);
+    }
+    T *slot = reinterpret_cast<T *>(reinterpret_cast<char *>(sc) + 64 * wid);
+    if (lane == kWave - 1) *slot = inc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      T acc = *reinterpret_cast<T *>(reinterpret_cast<char *>(sc));
+      for (int w = 1; w < kWaves; ++w) {
+        T *sw = reinterpret_cast<T *>(reinterpret_cast<char *>(sc) + 64 * w);
+        T t = *sw;
+        *sw = acc;
+        acc = op(acc, t);
+      }
+      *reinterpret_cast<T *>(reinterpret_cast<char *>(sc)) = identity;
+      *reinterpret_cast<T *>(reinterpret_cast<char *>(sc) + 64 * kWaves) = acc;
+    }
+    __syncthreads();
+    const T up = shfl_up(inc, 1);
+    const T wpre = *reinterpret_cast<T *>(reinterpret_cast<char *>(sc) + 64 * wid);
+    const T ex = lane == 0 ? wpre : op(wpre, up);
+    *total = *reinterpret_cast<T *>(reinterpret_cast<char *>(sc) + 64 * kWaves);
+    __syncthreads();
+    return ex;
+  }
+};
+
+// LDS bytes the policy needs
+constexpr int kBlockScratchU64 = 8 * (kWaves + 1);
+
+}  // namespace dmlc_amd

@@ -1,430 +1,19 @@
-// csv.hip -- MI355X kernels for CSVParser<I,D>::ParseBlock (src/data/csv_parser.h:71-149).
-//
-// Same tile/window decomposition as libsvm.hip: tile k owns the CSV line
-// starts in [k*T, (k+1)*T) (a line start is a non-'\n'/'\r' byte that follows
-// one, or a chunk's first such byte; a line that begins with a UTF-8 BOM
-// followed by a single line break absorbs the next line, text_parser.h:83-102,
-// csv_parser.h:83-87).
-//
-// Fast lines (no BOM, delimiter that no decoder can consume): every field is
-// decoded independently by the thread that owns its first byte; its column is
-// the number of delimiters since the line start, carried by a segmented block
-// scan.  Slow lines (BOM, or a whitespace / alphanumeric / sign delimiter,
-// where ParseFloat's whitespace skip changes the field structure) are parsed
-// by the owner of the line start with an exact sequential restatement of the
-// per-line loop (csv_parser.h:81-145).
-#include "decode.h"
+// csv.hip -- MI355X kernels for CSVParser<I,D>::ParseBlock (csv_parser.h:71-149);
+// the tile body lives in csv_core.h.
+#include "block.h"
+#include "csv_core.h"
 #include "dmlc_amd_kernels.h"
 #include "scan.h"
 
 namespace dmlc_amd {
-
 namespace {
-
-constexpr uint64_t kNone = ~0ull;
-
-struct Base64 {
-  uint64_t c[C_N];
-};
-
-// segmented column state: bit31 = reset (segment holds a line start),
-// bit30 = slow line, bits 0..29 = delimiters since the (last) line start
-struct ColCombine {
-  __device__ uint32_t operator()(uint32_t l, uint32_t r) const {
-    if (r & 0x80000000u) return r;
-    return (l & 0xC0000000u) | (((l & 0x3FFFFFFFu) + (r & 0x3FFFFFFFu)) & 0x3FFFFFFFu);
-  }
-};
-
-__device__ __forceinline__ bool is_bom_at(const Src &at, uint64_t p) {
-  return at(p) == 0xEFu && at(p + 1) == 0xBBu && at(p + 2) == 0xBFu;
-}
-
-// Exact CSV line-start predicate (see file comment).
-__device__ bool csv_line_start(const Src &at, uint64_t x, uint64_t cfloor) {
-  if (is_nl(at(x))) return false;
-  if (x != cfloor && !is_nl(at(x - 1))) return false;
-  // BOM units "EF BB BF <nl>" chained right before x: odd chain => x absorbed
-  int k = 0;
-  uint64_t y = x;
-  while (y >= cfloor + 4 && is_nl(at(y - 1)) && at(y - 4) == 0xEFu && at(y - 3) == 0xBBu &&
-         at(y - 2) == 0xBFu && (y - 4 == cfloor || is_nl(at(y - 5)))) {
-    ++k;
-    y -= 4;
-  }
-  return (k & 1) == 0;
-}
-
-template <typename T>
-__device__ __forceinline__ void store_val(void *arr, int vtype, uint64_t i, float f, int64_t v) {
-  if (vtype == 0) reinterpret_cast<float *>(arr)[i] = f;
-  else if (vtype == 1) reinterpret_cast<int32_t *>(arr)[i] = (int32_t)v;
-  else reinterpret_cast<int64_t *>(arr)[i] = v;
-}
-
-struct Field {
-  float f;
-  int64_t i;
-  uint64_t end;
-  bool nan_err;
-};
-
-__device__ __forceinline__ Field decode_field(const Src &at, int vtype, uint64_t p) {
-  Field r;
-  r.nan_err = false;
-  r.f = 0.f;
-  r.i = 0;
-  if (vtype == 0) {
-    r.f = parse_float(at, p, &r.end, &r.nan_err);
-  } else {
-    r.i = c_strtoll(at, p, 0, &r.end);
-    if (vtype == 1) r.i = (int64_t)(int32_t)r.i;
-  }
-  return r;
-}
-
-// csv_parser.h:81-145 for ONE line starting at `lbegin` (a CSV line start).
-template <int MODE>
-__device__ void csv_line_seq(const Src &at, const CsvArgs &a, uint64_t lbegin, uint64_t end, Cnt &cnt,
-                             const Base64 &base) {
-  {  // IgnoreUTF8BOM
-    int count = 0;
-    const uint32_t bom[3] = {0xEFu, 0xBBu, 0xBFu};
-    while (lbegin != end && count < 3 && at(lbegin) == bom[count]) {
-      ++count;
-      ++lbegin;
-    }
-    if (count < 3) lbegin -= count;
-  }
-  if (lbegin == end) return;  // reference reads past `end` here (UB); the oracle stops too
-  uint64_t lend = lbegin + 1;
-  while (lend != end && !is_nl(at(lend))) ++lend;
-  const uint64_t row = base.c[C_ROWS] + cnt.c[C_ROWS];
-  if (MODE == 2) {
-    if (row < a.cap[C_ROWS]) a.offset[row] = base.c[C_INDEX] + cnt.c[C_INDEX];
-    else raise_error(a.err, E_CAPACITY, lbegin);
-  }
-  uint64_t p = lbegin;
-  int col = 0;
-  uint64_t idx = 0;
-  float weight = __uint_as_float(0x7FC00000u);
-  while (p != lend) {
-    Field f = decode_field(at, a.vtype, p);
-    if (MODE == 2 && f.nan_err) raise_error(a.err, E_NAN_LITERAL, p);
-    if (col == a.label_column) {
-      if (MODE == 2) {
-        const uint64_t r = base.c[C_LABEL] + cnt.c[C_LABEL];
-        if (r < a.cap[C_LABEL]) store_val<int>(a.label, a.vtype, r, f.f, f.i);
-        else raise_error(a.err, E_CAPACITY, p);
-      }
-      cnt.c[C_LABEL]++;
-    } else if (a.vtype == 0 && col == a.weight_column) {
-      weight = f.f;
-    } else {
-      if (f.end != p) {
-        if (MODE == 2) {
-          const uint64_t r = base.c[C_INDEX] + cnt.c[C_INDEX];
-          const uint64_t rv = base.c[C_VALUE] + cnt.c[C_VALUE];
-          if (r < a.cap[C_INDEX] && rv < a.cap[C_VALUE]) {
-            store_val<int>(a.value, a.vtype, rv, f.f, f.i);
-            if (a.wide) reinterpret_cast<uint64_t *>(a.index)[r] = idx;
-            else reinterpret_cast<uint32_t *>(a.index)[r] = (uint32_t)idx;
-          } else {
-            raise_error(a.err, E_CAPACITY, p);
-          }
-        }
-        cnt.c[C_INDEX]++;
-        cnt.c[C_VALUE]++;
-      }
-      idx++;
-    }
-    p = f.end >= lend ? lend : f.end;
-    ++col;
-    while (at(p) != a.delim && p != lend) ++p;
-    if (p == lend && idx == 0) {
-      raise_error(a.err, E_CSV_DELIM, p);
-      return;
-    }
-    if (p != lend) ++p;
-  }
-  if (!(weight != weight)) {
-    if (MODE == 2) {
-      const uint64_t r = base.c[C_WEIGHT] + cnt.c[C_WEIGHT];
-      if (r < a.cap[C_WEIGHT]) a.weight[r] = weight;
-      else raise_error(a.err, E_CAPACITY, lbegin);
-    }
-    cnt.c[C_WEIGHT]++;
-  }
-  cnt.c[C_ROWS]++;
-}
-
-struct Seg {
-  uint64_t lo, hi;
-  uint32_t ls, dl, fs;  // line-start, delimiter, field-start masks
-  uint32_t slow;        // slow flag per line start bit
-  int chunk;
-};
-
-// value-column rank of column c (csv_parser.h:111-121: idx counts every column
-// that is neither the label nor (float only) the weight column)
-__device__ __forceinline__ uint64_t value_rank(const CsvArgs &a, uint64_t c) {
-  uint64_t r = c;
-  if (a.label_column >= 0 && (uint64_t)a.label_column < c) --r;
-  if (a.vtype == 0 && a.weight_column >= 0 && (uint64_t)a.weight_column < c) --r;
-  return r;
-}
-__device__ __forceinline__ bool is_value_col(const CsvArgs &a, uint64_t c) {
-  return (int64_t)c != a.label_column && !(a.vtype == 0 && (int64_t)c == a.weight_column);
-}
-
-template <int MODE>  // 1 count, 2 emit
-__device__ void walk(const CsvArgs &a, Src &src, const Seg &sg, uint32_t state, Cnt &cnt,
-                     const Base64 &base) {
-  uint32_t ev = sg.ls | sg.dl | sg.fs;
-  int chunk = sg.chunk;
-  uint64_t cend = a.cs[chunk + 1];
-  src.lim = cend;
-  uint64_t col = state & 0x3FFFFFFFu;
-  bool slow = (state >> 30) & 1u;
-  bool in_line = (state >> 31) & 1u;  // a line start has been seen (always true inside an extent)
-  while (ev) {
-    const int i = __builtin_ctz(ev);
-    ev &= ev - 1;
-    const uint64_t x = sg.lo + i;
-    while (x >= cend) {
-      ++chunk;
-      cend = a.cs[chunk + 1];
-      src.lim = cend;
-    }
-    if ((sg.ls >> i) & 1u) {
-      in_line = true;
-      col = 0;
-      slow = (sg.slow >> i) & 1u;
-      if (MODE == 2 && x == a.cs[chunk]) {
-        uint64_t *row = a.chunk_tab + (uint64_t)chunk * C_N;
-        for (int k = 0; k < C_N; ++k) row[k] = base.c[k] + cnt.c[k];
-      }
-      if (slow) {
-        csv_line_seq<MODE>(src, a, x, cend, cnt, base);
-      } else {
-        if (MODE == 2) {
-          const uint64_t r = base.c[C_ROWS] + cnt.c[C_ROWS];
-          if (r < a.cap[C_ROWS]) a.offset[r] = base.c[C_INDEX] + cnt.c[C_INDEX];
-          else raise_error(a.err, E_CAPACITY, x);
-        }
-        cnt.c[C_ROWS]++;
-      }
-    }
-    if (!in_line || slow) continue;
-    if ((sg.fs >> i) & 1u) {
-      Field f = decode_field(src, a.vtype, x);
-      if (MODE == 2 && f.nan_err) raise_error(a.err, E_NAN_LITERAL, x);
-      const bool vc = is_value_col(a, col);
-      if ((int64_t)col == a.label_column) {
-        if (MODE == 2) {
-          const uint64_t r = base.c[C_LABEL] + cnt.c[C_LABEL];
-          if (r < a.cap[C_LABEL]) store_val<int>(a.label, a.vtype, r, f.f, f.i);
-          else raise_error(a.err, E_CAPACITY, x);
-        }
-        cnt.c[C_LABEL]++;
-      } else if (!vc) {  // weight column (float)
-        if (!(f.f != f.f)) {
-          if (MODE == 2) {
-            const uint64_t r = base.c[C_WEIGHT] + cnt.c[C_WEIGHT];
-            if (r < a.cap[C_WEIGHT]) a.weight[r] = f.f;
-            else raise_error(a.err, E_CAPACITY, x);
-          }
-          cnt.c[C_WEIGHT]++;
-        }
-      } else if (f.end != x) {
-        if (MODE == 2) {
-          const uint64_t r = base.c[C_INDEX] + cnt.c[C_INDEX];
-          const uint64_t rv = base.c[C_VALUE] + cnt.c[C_VALUE];
-          if (r < a.cap[C_INDEX] && rv < a.cap[C_VALUE]) {
-            store_val<int>(a.value, a.vtype, rv, f.f, f.i);
-            const uint64_t ix = value_rank(a, col);
-            if (a.wide) reinterpret_cast<uint64_t *>(a.index)[r] = ix;
-            else reinterpret_cast<uint32_t *>(a.index)[r] = (uint32_t)ix;
-          } else {
-            raise_error(a.err, E_CAPACITY, x);
-          }
-        }
-        cnt.c[C_INDEX]++;
-        cnt.c[C_VALUE]++;
-      }
-      // csv_parser.h:128-132: after the line's last field, no value column seen
-      if (MODE == 2 && value_rank(a, col) + (vc ? 1 : 0) == 0) {
-        uint64_t p = x;
-        while (p < cend && !is_nl(src(p)) && src(p) != a.delim) ++p;
-        if (p >= cend || is_nl(src(p))) raise_error(a.err, E_CSV_DELIM, p);
-      }
-    }
-    if ((sg.dl >> i) & 1u) ++col;
-  }
-}
-
-__device__ uint64_t first_line_start(const CsvArgs &a, uint64_t from, uint64_t to, uint64_t *scratch) {
-  Src src;
-  src.g = a.text;
-  src.lds = nullptr;
-  src.wbase = src.wend = 0;
-  for (uint64_t base = from; base < to; base += kWin) {
-    uint64_t best = kNone;
-    const uint64_t lo = base + (uint64_t)threadIdx.x * kSeg;
-    const uint64_t hi = min(lo + kSeg, to);
-    if (lo < hi) {
-      int c = chunk_of(a.cs, a.nchunk, lo);
-      for (uint64_t p = lo; p < hi; ++p) {
-        while (p >= a.cs[c + 1]) ++c;
-        src.lim = a.cs[c + 1];
-        if (csv_line_start(src, p, a.cs[c])) {
-          best = p;
-          break;
-        }
-      }
-    }
-    best = block_min(best, scratch);
-    if (best != kNone) return best;
-  }
-  return kNone;
-}
 
 template <int MODE>
 __global__ void __launch_bounds__(kThreads) csv_tile(CsvArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t win[kWin + 32];
-  __shared__ uint32_t scol[kWaves + 1];
-  __shared__ Cnt scnt[kWaves + 1];
-  __shared__ uint64_t s64[kWaves + 1];
-
-  const uint64_t k = blockIdx.x;
-  const uint64_t tlo = k * a.tile_bytes;
-  if (tlo >= a.n) return;
-  const uint64_t thi = min(tlo + a.tile_bytes, a.n);
-  const int tid = threadIdx.x;
-  Cnt zero;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) zero.c[i] = 0;
-  Cnt tot = zero, mine = zero;
-  Base64 tbase;
-#pragma unroll
-  for (int i = 0; i < C_N; ++i) tbase.c[i] = MODE == 2 ? a.tile_base[k * C_N + i] : 0;
-
-  uint64_t w0 = first_line_start(a, tlo, a.n, s64);
-  if (w0 == kNone || w0 >= thi) {
-    if (MODE == 1 && tid < C_N) a.tile_cnt[k * C_N + tid] = 0;
-    return;
-  }
-  uint32_t col0 = 0;  // column state at the window start (window 0 starts at a line start)
-  bool done = false;
-  Src src;
-  src.g = a.text;
-  src.lds = win;
-  while (!done) {
-    uint64_t wend = min(w0 + (uint64_t)kWin, a.n);
-    if (wend == a.n) done = true;
-    if (wend > thi) {
-      const uint64_t e = first_line_start(a, max(w0, thi), wend, s64);
-      if (e != kNone) {
-        wend = e;
-        done = true;
-      }
-    }
-    if (wend == w0) break;
-    const uint64_t abase = w0 & ~15ull;
-    const uint64_t nunits = (wend - abase + 15) >> 4;
-    for (uint64_t u = tid; u < nunits; u += kThreads) {
-      const uint64_t g = abase + (u << 4);
-      if (g + 16 <= a.n) {
-        *reinterpret_cast<uint4 *>(&win[u << 4]) = *reinterpret_cast<const uint4 *>(a.text + g);
-      } else {
-        for (int j = 0; j < 16; ++j) win[(u << 4) + j] = g + j < a.n ? a.text[g + j] : 0;
-      }
-    }
-    __syncthreads();
-    src.wbase = abase;
-    src.wend = min(abase + (nunits << 4), a.n);
-
-    Seg sg;
-    sg.lo = w0 + (uint64_t)tid * kSeg;
-    sg.hi = min(sg.lo + kSeg, wend);
-    sg.ls = sg.dl = sg.fs = sg.slow = 0;
-    sg.chunk = 0;
-    uint32_t summary = 0;  // ColCombine element
-    if (sg.lo < sg.hi) {
-      sg.chunk = chunk_of(a.cs, a.nchunk, sg.lo);
-      int c = sg.chunk;
-      src.lim = a.cs[c + 1];
-      const int len = (int)(sg.hi - sg.lo);
-      uint32_t nl = 0, dl = 0, ls = 0;
-      for (int i = 0; i < len; ++i) {
-        const uint32_t ch = win[sg.lo + i - abase];
-        nl |= (uint32_t)is_nl(ch) << i;
-        dl |= (uint32_t)(ch == a.delim) << i;
-      }
-      // line starts: non-nl byte after an nl byte (or a chunk start), minus absorbed
-      const uint32_t prev_nl = (sg.lo == 0 || is_nl(src(sg.lo - 1))) ? 1u : 0u;
-      uint32_t cand = ~nl & ((nl << 1) | prev_nl);
-      if (len < 32) cand &= (1u << len) - 1u;
-      for (int cc = c; cc < a.nchunk && a.cs[cc] < sg.hi; ++cc)
-        if (a.cs[cc] >= sg.lo && !((nl >> (a.cs[cc] - sg.lo)) & 1u)) cand |= 1u << (a.cs[cc] - sg.lo);
-      uint32_t m = cand;
-      while (m) {
-        const int i = __builtin_ctz(m);
-        m &= m - 1;
-        const uint64_t x = sg.lo + i;
-        while (x >= a.cs[c + 1]) ++c;
-        src.lim = a.cs[c + 1];
-        if (csv_line_start(src, x, a.cs[c])) {
-          ls |= 1u << i;
-          if (!a.fast_delim || is_bom_at(src, x)) sg.slow |= 1u << i;
-        }
-      }
-      src.lim = a.cs[sg.chunk + 1];
-      sg.ls = ls;
-      sg.dl = dl & ~nl;
-      // field starts: line starts of fast lines, and bytes after a delimiter that are not nl
-      const uint32_t prev_dl = (sg.lo > 0 && src(sg.lo - 1) == a.delim && !(ls & 1u)) ? 1u : 0u;
-      uint32_t fs = ((sg.dl << 1) | prev_dl) & ~nl;
-      if (len < 32) fs &= (1u << len) - 1u;
-      sg.fs = fs | (ls & ~sg.slow);
-      if (ls) {
-        const int last = 31 - __builtin_clz(ls);
-        const uint32_t after = last == 31 ? 0u : (sg.dl & ~((2u << last) - 1u));
-        summary = 0x80000000u | (((sg.slow >> last) & 1u) << 30) | (uint32_t)__builtin_popcount(after);
-      } else {
-        summary = (uint32_t)__builtin_popcount(sg.dl);
-      }
-    }
-    uint32_t col_total;
-    const uint32_t col_ex = block_exclusive(summary, 0u, ColCombine(), scol, &col_total);
-    const uint32_t in_state = ColCombine()(col0 | 0x80000000u, col_ex);
-    const uint32_t next0 = ColCombine()(col0 | 0x80000000u, col_total);
-
-    Cnt cc = zero;
-    if (sg.lo < sg.hi) walk<1>(a, src, sg, in_state, cc, Base64());
-    if (MODE == 1) {
-      mine = CntAdd()(mine, cc);
-    } else {
-      Cnt wtot;
-      const Cnt ex = block_exclusive(cc, zero, CntAdd(), scnt, &wtot);
-      if (sg.lo < sg.hi) {
-        Base64 b;
-#pragma unroll
-        for (int i = 0; i < C_N; ++i) b.c[i] = tbase.c[i] + tot.c[i] + ex.c[i];
-        Cnt local = zero;
-        walk<2>(a, src, sg, in_state, local, b);
-      }
-      tot = CntAdd()(tot, wtot);
-    }
-    col0 = next0 & 0x7FFFFFFFu;
-    w0 = wend;
-    __syncthreads();
-  }
-  if (MODE == 1) {
-    Cnt total;
-    (void)block_exclusive(mine, zero, CntAdd(), scnt, &total);
-    if (tid < C_N) a.tile_cnt[k * C_N + tid] = total.c[tid];
-  }
+  __shared__ __attribute__((aligned(16))) csv::Shared sh;
+  __shared__ uint64_t scratch[kBlockScratchU64];
+  DevBlock bk{scratch};
+  csv::tile<MODE>(a, sh, bk, blockIdx.x);
 }
 
 __global__ void finalize_kernel(uint64_t *res) {

@@ -17,7 +17,7 @@
 namespace dmlc_amd {
 
 template <typename F>
-__device__ __forceinline__ float parse_float(const F &at, uint64_t p, uint64_t *endp, bool *nan_err) {
+DA_HD float parse_float(const F &at, uint64_t p, uint64_t *endp, bool *nan_err) {
   while (is_space(at(p))) ++p;
   bool sign = true;
   uint32_t c = at(p);
@@ -52,7 +52,7 @@ __device__ __forceinline__ float parse_float(const F &at, uint64_t p, uint64_t *
         ++p;
       }
       *endp = p;
-      return __uint_as_float(0x7FC00000u);
+      return u2f(0x7FC00000u);
     }
   }
   uint64_t predec = 0;
@@ -103,7 +103,7 @@ __device__ __forceinline__ float parse_float(const F &at, uint64_t p, uint64_t *
 
 // Returns false on a leading '-' (the reference's fatal CHECK).
 template <typename F>
-__device__ __forceinline__ bool parse_uint(const F &at, uint64_t p, bool wide, uint64_t *out) {
+DA_HD bool parse_uint(const F &at, uint64_t p, bool wide, uint64_t *out) {
   uint32_t c = at(p);
   while (is_space(c)) c = at(++p);
   if (c == '-') return false;
@@ -123,7 +123,7 @@ __device__ __forceinline__ bool parse_uint(const F &at, uint64_t p, bool wide, u
 // glibc strtoll, C locale, base 10 or 0 (auto 0x / 0 prefixes), saturating.
 // *endp = first unconsumed byte, or `p` itself when no digits were consumed.
 template <typename F>
-__device__ __forceinline__ int64_t c_strtoll(const F &at, uint64_t p0, int base, uint64_t *endp) {
+DA_HD int64_t c_strtoll(const F &at, uint64_t p0, int base, uint64_t *endp) {
   uint64_t p = p0;
   uint32_t c = at(p);
   while (is_cspace(c)) c = at(++p);

@@ -1,7 +1,7 @@
 // scan.h -- exclusive scan of per-tile counter vectors (single workgroup) and
 // pipeline finalisation.  Included by each kernel translation unit (no RDC).
 #pragma once
-#include "common.h"
+#include "block.h"
 
 namespace dmlc_amd {
 namespace {  // one private copy per kernel translation unit (no RDC)
@@ -10,7 +10,7 @@ struct Cnt64 {
   uint64_t c[8];
 };
 struct Cnt64Add {
-  __device__ Cnt64 operator()(const Cnt64 &a, const Cnt64 &b) const {
+  DA_HD Cnt64 operator()(const Cnt64 &a, const Cnt64 &b) const {
     Cnt64 r;
 #pragma unroll
     for (int i = 0; i < 8; ++i) r.c[i] = a.c[i] + b.c[i];
@@ -23,7 +23,8 @@ struct Cnt64Add {
 __global__ void __launch_bounds__(kThreads)
 tile_scan_kernel(const uint64_t *tile_cnt, uint64_t *tile_base, uint32_t ntiles, uint64_t *res,
                  uint64_t *offset, uint64_t cap_rows) {
-  __shared__ Cnt64 sc[kWaves + 1];
+  __shared__ uint64_t scratch[kBlockScratchU64];
+  DevBlock bk{scratch};
   const uint32_t per = (ntiles + kThreads - 1) / kThreads;
   const uint32_t t0 = threadIdx.x * per, t1 = min(t0 + per, ntiles);
   Cnt64 mine, zero;
@@ -32,7 +33,7 @@ tile_scan_kernel(const uint64_t *tile_cnt, uint64_t *tile_base, uint32_t ntiles,
   for (uint32_t k = t0; k < t1; ++k)
     for (int i = 0; i < C_N; ++i) mine.c[i] += tile_cnt[(uint64_t)k * C_N + i];
   Cnt64 total;
-  Cnt64 run = block_exclusive(mine, zero, Cnt64Add(), sc, &total);
+  Cnt64 run = bk.exclusive(mine, zero, Cnt64Add(), &total);
   for (uint32_t k = t0; k < t1; ++k)
     for (int i = 0; i < C_N; ++i) {
       tile_base[(uint64_t)k * C_N + i] = run.c[i];

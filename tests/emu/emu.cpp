@@ -1,0 +1,284 @@
+// emu.cpp -- TEST INFRASTRUCTURE ONLY: CPU emulation of the HIP tile kernels.
+//
+// Runs the exact per-thread tile bodies of dmlc-core_amd/csrc/{libsvm,csv}_core.h
+// with 256 std::threads per workgroup, a real barrier and a serial block scan,
+// so kernel logic can be debugged (and run under AddressSanitizer) without a
+// GPU.  Never part of the product: nothing in dmlc-core_amd/ links it.
+#include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "csv_core.h"
+#include "dmlc_amd.h"
+#include "libsvm_core.h"
+
+using namespace dmlc_amd;
+
+namespace {
+
+struct Barrier {
+  std::mutex m;
+  std::condition_variable cv;
+  int n, waiting = 0;
+  unsigned gen = 0;
+  explicit Barrier(int n_) : n(n_) {}
+  void wait() {
+    std::unique_lock<std::mutex> lk(m);
+    const unsigned g = gen;
+    if (++waiting == n) {
+      waiting = 0;
+      ++gen;
+      cv.notify_all();
+    } else {
+      cv.wait(lk, [&] { return gen != g; });
+    }
+  }
+};
+
+struct BlockCtx {
+  Barrier bar{kThreads};
+  alignas(64) unsigned char scan[kThreads * 64];
+  uint64_t mins[kThreads];
+};
+
+struct HostBlock {
+  int t;
+  BlockCtx *ctx;
+  int tid() const { return t; }
+  void sync() { ctx->bar.wait(); }
+  uint64_t min_u64(uint64_t v) {
+    ctx->mins[t] = v;
+    sync();
+    uint64_t r = ~0ull;
+    for (int i = 0; i < kThreads; ++i) r = ctx->mins[i] < r ? ctx->mins[i] : r;
+    sync();
+    return r;
+  }
+  template <typename T, typename Op>
+  T exclusive(T v, T identity, Op op, T *total) {
+    static_assert(sizeof(T) <= 64, "scan element");
+    T *buf = reinterpret_cast<T *>(ctx->scan);
+    buf[t] = v;
+    sync();
+    T acc = identity;
+    for (int i = 0; i < t; ++i) acc = op(acc, buf[i]);
+    T all = acc;
+    for (int i = t; i < kThreads; ++i) all = op(all, buf[i]);
+    *total = all;
+    sync();
+    return acc;
+  }
+};
+
+template <typename Body>
+void run_block(Body body) {
+  BlockCtx ctx;
+  std::vector<std::thread> th;
+  th.reserve(kThreads);
+  for (int t = 0; t < kThreads; ++t)
+    th.emplace_back([&, t] {
+      HostBlock bk{t, &ctx};
+      body(bk);
+    });
+  for (auto &x : th) x.join();
+}
+
+void tile_scan(const std::vector<uint64_t> &cnt, std::vector<uint64_t> &base, uint64_t ntiles, uint64_t *res) {
+  uint64_t run[C_N] = {0};
+  for (uint64_t k = 0; k < ntiles; ++k)
+    for (int i = 0; i < C_N; ++i) {
+      base[k * C_N + i] = run[i];
+      run[i] += cnt[k * C_N + i];
+    }
+  for (int i = 0; i < C_N; ++i) res[i] = run[i];
+}
+
+}  // namespace
+
+extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *cs, int nchunks,
+                         const dmlc_amd_params *prm, const dmlc_amd_csr *out, uint64_t *chunk_table,
+                         uint64_t *res /* 16 */) {
+  const uint64_t T = prm->tile_bytes ? prm->tile_bytes : (256ull << 10);
+  const uint64_t ntiles = (nbytes + T - 1) / T;
+  const bool count_only = prm->flags & DMLC_AMD_FLAG_COUNT_ONLY;
+  std::memset(res, 0, 16 * 8);
+  res[8] = ~0ull;
+  std::vector<uint64_t> tile_cnt(ntiles * C_N + 1), tile_base(ntiles * C_N + 1);
+  std::vector<uint64_t> chunk_min(nchunks > 0 ? nchunks : 1, ~0ull), sink((nchunks > 0 ? nchunks : 1) * 8);
+  unsigned long long *err = reinterpret_cast<unsigned long long *>(res + 8);
+  if (!ntiles && !count_only && out->offset) out->offset[0] = 0;
+  if (prm->format == DMLC_AMD_LIBSVM) {
+    LibsvmArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.text = text;
+    a.n = nbytes;
+    a.cs = cs;
+    a.nchunk = nchunks;
+    a.tile_bytes = T;
+    a.ntiles = (uint32_t)ntiles;
+    a.wide = prm->index_bits == 64;
+    a.indexing_mode = prm->indexing_mode;
+    a.tile_cnt = tile_cnt.data();
+    a.tile_base = tile_base.data();
+    a.offset = out->offset;
+    a.label = reinterpret_cast<float *>(out->label);
+    a.weight = out->weight;
+    a.qid = out->qid;
+    a.index = out->index;
+    a.value = reinterpret_cast<float *>(out->value);
+    for (int i = 0; i < 8; ++i) a.cap[i] = out->cap[i];
+    a.chunk_tab = chunk_table ? chunk_table : sink.data();
+    a.chunk_min = chunk_min.data();
+    a.err = err;
+    for (uint64_t k = 0; k < ntiles; ++k) {
+      svm::Shared *sh = new svm::Shared;
+      std::memset(sh, 0xCD, sizeof(*sh));  // LDS is uninitialised on the GPU
+      run_block([&](HostBlock &bk) { svm::tile<1>(a, *sh, bk, k); });
+      delete sh;
+    }
+    tile_scan(tile_cnt, tile_base, ntiles, res);
+    if (!count_only && out->offset && res[C_ROWS] < out->cap[C_ROWS] + 1) out->offset[res[C_ROWS]] = res[C_INDEX];
+    if (!count_only)
+      for (uint64_t k = 0; k < ntiles; ++k) {
+        svm::Shared *sh = new svm::Shared;
+        std::memset(sh, 0xCD, sizeof(*sh));
+        run_block([&](HostBlock &bk) { svm::tile<2>(a, *sh, bk, k); });
+        delete sh;
+      }
+  } else if (prm->format == DMLC_AMD_CSV) {
+    CsvArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.text = text;
+    a.n = nbytes;
+    a.cs = cs;
+    a.nchunk = nchunks;
+    a.tile_bytes = T;
+    a.ntiles = (uint32_t)ntiles;
+    a.wide = prm->index_bits == 64;
+    a.vtype = prm->value_type;
+    a.label_column = prm->label_column;
+    a.weight_column = prm->weight_column;
+    a.delim = (uint32_t)prm->delimiter & 0xFFu;
+    {
+      const unsigned c = a.delim;
+      a.fast_delim = !(c == ' ' || (c >= '\t' && c <= '\r') || (c >= '0' && c <= '9') ||
+                       ((c | 32u) >= 'a' && (c | 32u) <= 'z') || c == '+' || c == '-' || c == '.' ||
+                       c == '_' || c == '(' || c == ')' || c == 0);
+    }
+    a.tile_cnt = tile_cnt.data();
+    a.tile_base = tile_base.data();
+    a.offset = out->offset;
+    a.label = out->label;
+    a.weight = out->weight;
+    a.index = out->index;
+    a.value = out->value;
+    for (int i = 0; i < 8; ++i) a.cap[i] = out->cap[i];
+    a.chunk_tab = chunk_table ? chunk_table : sink.data();
+    a.err = err;
+    for (uint64_t k = 0; k < ntiles; ++k) {
+      csv::Shared *sh = new csv::Shared;
+      std::memset(sh, 0xCD, sizeof(*sh));
+      run_block([&](HostBlock &bk) { csv::tile<1>(a, *sh, bk, k); });
+      delete sh;
+    }
+    tile_scan(tile_cnt, tile_base, ntiles, res);
+    if (!count_only && out->offset && res[C_ROWS] < out->cap[C_ROWS] + 1) out->offset[res[C_ROWS]] = res[C_INDEX];
+    if (!count_only)
+      for (uint64_t k = 0; k < ntiles; ++k) {
+        csv::Shared *sh = new csv::Shared;
+        std::memset(sh, 0xCD, sizeof(*sh));
+        run_block([&](HostBlock &bk) { csv::tile<2>(a, *sh, bk, k); });
+        delete sh;
+      }
+  } else {
+    return DMLC_AMD_ERR_ARG;
+  }
+  if (res[8] == ~0ull) res[8] = 0;
+  return 0;
+}
+
+// ---------------------------------------------------------------- CLI mode
+// emu <fmt> <index_bits> <vtype> <indexing_mode> <label_col> <weight_col> <delim_code> <tile>
+//     <text_file> <chunks_file (uint64 LE, nchunks+1)> <out_prefix>
+// Writes <out_prefix>.{res,offset,label,weight,qid,index,value,chunks} raw little-endian.
+static std::vector<char> slurp(const char *p) {
+  FILE *f = std::fopen(p, "rb");
+  if (!f) return {};
+  std::vector<char> v;
+  char buf[1 << 16];
+  size_t n;
+  while ((n = std::fread(buf, 1, sizeof(buf), f)) > 0) v.insert(v.end(), buf, buf + n);
+  std::fclose(f);
+  return v;
+}
+static void dump(const std::string &p, const void *d, size_t n) {
+  FILE *f = std::fopen(p.c_str(), "wb");
+  if (n) std::fwrite(d, 1, n, f);
+  std::fclose(f);
+}
+
+int main(int argc, char **argv) {
+  if (argc != 12) {
+    std::fprintf(stderr, "usage: see source\n");
+    return 2;
+  }
+  dmlc_amd_params prm;
+  std::memset(&prm, 0, sizeof(prm));
+  prm.format = std::atoi(argv[1]);
+  prm.index_bits = std::atoi(argv[2]);
+  prm.value_type = std::atoi(argv[3]);
+  prm.indexing_mode = std::atoi(argv[4]);
+  prm.label_column = std::atoi(argv[5]);
+  prm.weight_column = std::atoi(argv[6]);
+  prm.delimiter = std::atoi(argv[7]);
+  prm.tile_bytes = (uint32_t)std::atoi(argv[8]);
+  std::vector<char> text = slurp(argv[9]);
+  std::vector<char> craw = slurp(argv[10]);
+  std::vector<uint64_t> cs(craw.size() / 8);
+  std::memcpy(cs.data(), craw.data(), craw.size());
+  const int nch = (int)cs.size() - 1;
+  // exact-size heap copy of the text so ASan sees reads past its end
+  uint8_t *t = (uint8_t *)std::malloc(text.size() ? text.size() : 1);
+  std::memcpy(t, text.data(), text.size());
+  uint64_t res[16];
+  dmlc_amd_csr csr;
+  std::memset(&csr, 0, sizeof(csr));
+  prm.flags = DMLC_AMD_FLAG_COUNT_ONLY;
+  emu_parse(t, text.size(), cs.data(), nch, &prm, &csr, nullptr, res);
+  prm.flags = 0;
+  const size_t vsz = prm.value_type == DMLC_AMD_I64 ? 8 : 4, isz = prm.index_bits == 64 ? 8 : 4;
+  std::vector<uint64_t> offset(res[0] + 1);
+  void *label = std::malloc(res[5] * vsz + 1), *value = std::malloc(res[2] * vsz + 1),
+       *index = std::malloc(res[1] * isz + 1);
+  std::vector<float> weight(res[3] + 1);
+  std::vector<uint64_t> qid(res[4] + 1);
+  std::vector<uint64_t> chunks((nch > 0 ? nch : 1) * 8, 0);
+  csr.offset = offset.data();
+  csr.label = label;
+  csr.weight = weight.data();
+  csr.qid = qid.data();
+  csr.index = index;
+  csr.value = value;
+  uint64_t caps[8] = {res[0], res[1], res[2], res[3], res[4], res[5], res[6], 0};
+  std::memcpy(csr.cap, caps, sizeof(caps));
+  uint64_t res2[16];
+  emu_parse(t, text.size(), cs.data(), nch, &prm, &csr, chunks.data(), res2);
+  std::string o = argv[11];
+  dump(o + ".res", res2, sizeof(res2));
+  dump(o + ".offset", offset.data(), offset.size() * 8);
+  dump(o + ".label", label, res2[5] * vsz);
+  dump(o + ".weight", weight.data(), res2[3] * 4);
+  dump(o + ".qid", qid.data(), res2[4] * 8);
+  dump(o + ".index", index, res2[1] * isz);
+  dump(o + ".value", value, res2[2] * vsz);
+  dump(o + ".chunks", chunks.data(), chunks.size() * 8);
+  std::free(t);
+  std::free(label);
+  std::free(value);
+  std::free(index);
+  return 0;
+}

@@ -1,0 +1,93 @@
+"""CPU runs of the kernel tile bodies (test-only emulator, ASan) vs goldens/oracle.
+
+The emulator executes the same per-thread code as the HIP kernels
+(dmlc-core_amd/csrc/*_core.h) with 256 host threads per workgroup; these tests
+catch logic and memory-safety bugs in the kernel bodies without a GPU."""
+import numpy as np
+import pytest
+
+from golden_util import dec, diff, load_cases
+from oracle import pyoracle as po
+from tests.emu import pyemu
+
+FMT = {po.LIBSVM: "libsvm", po.CSV: "csv"}
+
+
+def check_fail(h, fmt, offs):
+    import dmlc_amd
+    nch = len(offs) - 1
+    return bool(h["error"]) or (nch > 0 and dmlc_amd.chunk_check(h, fmt, nch, h["counts"]) >= 0)
+
+
+def kw_of(params):
+    kw = {}
+    for k, v in params.items():
+        if k in ("fmt", "nthread"):
+            continue
+        kw["value_type" if k == "value_kind" else k] = v
+    return kw
+
+
+CASES = [c for c in load_cases() if c["params"]["fmt"] in FMT]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
+def test_emu_goldens(case):
+    prm = case["params"]
+    data = case["data_latin1"].encode("latin-1")
+    offs = [0, len(data)] if data else [0]
+    h = pyemu.parse(data, offs, FMT[prm["fmt"]], **kw_of(prm))
+    failed = check_fail(h, FMT[prm["fmt"]], offs)
+    if case["status"]:
+        assert failed
+        return
+    assert not failed, h["error"]
+    exp = {k: dec(v) for k, v in case["expect"].items()}
+    assert diff(h, exp) == []
+
+
+def _fuzz(rng, fmt):
+    alpha = {po.LIBSVM: list("0123456789") * 6 + list("  ::.-+eE#\tq") + ["qid:", "nan", "inf", "\r"],
+             po.CSV: list("0123456789") * 6 + list(",,,,.-+eE \t") + ["nan", "inf", "0x", "\xef\xbb\xbf"]}[fmt]
+    lines = ["".join(alpha[int(i)] for i in rng.integers(0, len(alpha), int(rng.integers(0, 60))))
+             for _ in range(int(rng.integers(1, 10)))]
+    t = "\n".join(lines) + ("\n" if rng.random() < 0.5 else "")
+    return t.encode("latin-1")
+
+
+@pytest.mark.parametrize("fmt", [po.LIBSVM, po.CSV])
+def test_emu_fuzz_vs_oracle(fmt):
+    rng = np.random.default_rng(99 + fmt)
+    for it in range(60):
+        data = _fuzz(rng, fmt)
+        nl = [i + 1 for i, b in enumerate(data) if b in (10, 13) and i + 1 < len(data)]
+        cuts = sorted(set(rng.choice(nl, size=min(len(nl), int(rng.integers(0, 3))), replace=False).tolist())) if nl else []
+        offs = [0] + cuts + [len(data)]
+        kw = {}
+        if rng.random() < 0.4:
+            kw["tile_bytes"] = int(rng.integers(8, 64))
+        if fmt == po.CSV and rng.random() < 0.3:
+            kw["label_column"] = int(rng.integers(0, 3))
+        if fmt == po.LIBSVM and rng.random() < 0.3:
+            kw["indexing_mode"] = int(rng.integers(-1, 2))
+        okw = {k: v for k, v in kw.items() if k != "tile_bytes"}
+        o = po.parse_chunks(data, offs, fmt=fmt, **okw)
+        h = pyemu.parse(data, offs, FMT[fmt], **kw)
+        failed = check_fail(h, FMT[fmt], offs)
+        assert (o["status"] != 0) == failed, (it, data, offs, kw, o["msg"], h["error"])
+        if not failed:
+            assert diff(h, o) == [], (it, data, offs, kw, diff(h, o))
+
+
+def test_emu_long_lines_small_tiles():
+    rng = np.random.default_rng(3)
+    lines = []
+    for r in range(5):
+        k = int(rng.integers(200, 1500))
+        lines.append("%d%s %s" % (r % 2, " qid:%d" % r if r % 2 else "",
+                                  " ".join("%d:%.6g" % (i, rng.random()) for i in range(k))))
+    data = ("\n".join(lines) + "\n").encode()
+    for tile in (0, 5000, 20000):
+        o = po.parse_chunks(data, [0, len(data)], fmt=po.LIBSVM)
+        h = pyemu.parse(data, [0, len(data)], "libsvm", tile_bytes=tile)
+        assert h["error"] == 0 and diff(h, o) == []
