@@ -1,0 +1,225 @@
+"""Device-resident libsvm / CSV parse throughput on MI355X (BASELINE.json metric).
+
+One step = one full pass of the parse pipeline (count phase -> scan -> write
+phase, i.e. dmlc_amd_parse with COUNT_ONLY then FILL_ONLY, which together do
+exactly the work of one full call) over this rank's HBM-resident synthetic
+shard, into pre-allocated CSR outputs.  The text is made by the canonical
+generator (tools/synth.c, splitmix64) and chunked exactly as dmlc-core's text
+InputSplit would chunk it (8 MiB buffers cut after the last newline).
+
+Multi-GPU (torchrun, one process per GPU): every rank parses its own shard of
+rows (rank * rows .. (rank + 1) * rows); there is no data-path collective (the
+reference's DP byte-range split exchanges nothing).  torch.distributed is used
+only for the start/stop barriers and the max-over-ranks time.
+
+Output: one JSON line on rank 0 (see DESIGN.md "Measurement").
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (ROOT, os.path.join(ROOT, "dmlc-core_amd", "python")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import dmlc_amd  # noqa: E402
+from tools import synth  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
+
+# name -> (format, rows per GPU, width, BASELINE.json config index)
+CONFIGS = {
+    "libsvm_1m_x128": ("libsvm", 1 << 20, 128, 1),
+    "csv_1m_x256": ("csv", 1 << 20, 256, 2),
+    "libsvm_1m_x2048": ("libsvm", 1 << 20, 2048, 3),
+    "libsvm_32m_x64": ("libsvm", 32 << 20, 64, 4),
+}
+DESC = {
+    "libsvm_1m_x128": "libsvm 1M rows x 128 nnz/row, device-resident",
+    "csv_1m_x256": "CSV dense 1M rows x 256 float cols, device-resident",
+    "libsvm_1m_x2048": "libsvm 1M rows x 2048 nnz/row, device-resident",
+    "libsvm_32m_x64": "libsvm 32M rows x 64 nnz/row, chunks sharded across GPUs",
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def csr_bytes(counts, index_bits=32, vbytes=4):
+    c = [int(x) for x in counts]
+    ib = index_bits // 8
+    return (8 * (c[dmlc_amd.ROWS] + 1) + vbytes * c[dmlc_amd.LABEL] + 4 * c[dmlc_amd.WEIGHT]
+            + 8 * c[dmlc_amd.QID] + ib * c[dmlc_amd.FIELD] + ib * c[dmlc_amd.INDEX]
+            + vbytes * c[dmlc_amd.VALUE])
+
+
+def cpu_baseline(text, starts, fmt, budget_s):
+    """Reference CPU parser (oracle/_ref when it travelled here, else the C
+    restatement) over a bounded prefix of this shard's chunks."""
+    from oracle import pyoracle as po
+    f = po.LIBSVM if fmt == "libsvm" else po.CSV
+    nproc = os.cpu_count() or 1
+    use_ref = po.ref_available()
+    # the reference's thread cap: min(max(nprocs/2 - 4, 1), nthread=2), text_parser.h:33-34, data.cc:31
+    nthread = min(max(nproc // 2 - 4, 1), 2) if use_ref else 1
+    # probe on 4 chunks, then size the sample to ~budget_s
+    k0 = min(4, len(starts) - 1)
+    t, _, _, _ = po.bench_chunks(text, starts[:k0 + 1], f, nthread, use_ref)
+    per_chunk = t / max(k0, 1)
+    k = int(min(len(starts) - 1, max(k0, budget_s / max(per_chunk, 1e-9))))
+    secs, nnz, kind, thr = po.bench_chunks(text, starts[:k + 1], f, nthread, use_ref)
+    nb = int(starts[k])
+    return {"value": round(nb / secs / 1e9, 4), "unit": "GB/s", "cores": thr, "kind": kind,
+            "sample": "%d of %d InputSplit chunks (%.1f MB, %d nnz) of the same shard, "
+                      "ParseBlock per chunk, %d thread(s) (reference cap min(max(nproc/2-4,1),2), "
+                      "nproc=%d), %.1f s" % (k, len(starts) - 1, nb / 1e6, nnz, thr, thr, nproc,
+                                             secs)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="libsvm_1m_x128", choices=sorted(CONFIGS))
+    ap.add_argument("--rows", type=int, default=0, help="override rows per GPU")
+    ap.add_argument("--tile-bytes", type=int, default=0)
+    ap.add_argument("--cpu-budget", type=float, default=15.0,
+                    help="seconds of CPU-baseline parsing (rank 0, N=1)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    fmt, rows, width, cfg_idx = CONFIGS[args.config]
+    if args.config == "libsvm_32m_x64":
+        rows = rows // max(world, args.gpus, 1) if world > 1 else rows // 8
+    if args.rows:
+        rows = args.rows
+    t0 = time.time()
+    text, _ = synth.rows(synth.LIBSVM if fmt == "libsvm" else synth.CSV, rows, width, seed=1,
+                         row0=rank * rows)
+    starts = dmlc_amd.text_chunk_starts(text)
+    log("[rank %d] generated %s: %d rows, %.3f GB, %d chunks in %.1f s"
+        % (rank, args.config, rows, text.size / 1e9, len(starts) - 1, time.time() - t0))
+
+    d_text = torch.from_numpy(text).to(dev)
+    d_starts = torch.from_numpy(starts).to(dev)
+    nbytes = int(text.size)
+    p = dmlc_amd.DeviceParser(fmt, tile_bytes=args.tile_bytes)
+    res = torch.zeros(16, dtype=torch.int64, device=dev)
+    counts = p.count(d_text, d_starts, result=res)
+    out = p.alloc(counts)
+    out["_csr"] = p.csr_of(out)
+    b_out = csr_bytes(counts)
+    s = torch.cuda.current_stream()
+
+    def step(evs=None):
+        if evs:
+            evs[0].record(s)
+        p.count_async(d_text, d_starts, res, out=out)
+        if evs:
+            evs[1].record(s)
+        p.fill_async(d_text, d_starts, out, res)
+        if evs:
+            evs[2].record(s)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    r = res.cpu().numpy().view(np.uint64)
+    if int(r[8]) != 0:
+        raise RuntimeError("parse error %#x" % int(r[8]))
+    if [int(x) for x in r[:7]] != [int(x) for x in counts[:7]]:
+        raise RuntimeError("count mismatch between phases")
+
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for k in range(args.steps):
+        step(evs[k])
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    count_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
+    fill_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
+    r = res.cpu().numpy().view(np.uint64)
+    if int(r[8]) != 0:
+        raise RuntimeError("parse error %#x" % int(r[8]))
+
+    ms_per_step = elapsed * 1e3 / args.steps
+    total_in = nbytes * world
+    value = total_in * args.steps / elapsed / 1e9
+    # dominant kernel: the write pass reads the text and writes the CSR (B_in + B_out);
+    # the count pass reads the text (B_in)
+    if fill_ms >= count_ms:
+        dom, dom_ms, dom_bytes = "%s_tile<2> (write pass)" % fmt, fill_ms, nbytes + b_out
+    else:
+        dom, dom_ms, dom_bytes = "%s_tile<1> (count pass)" % fmt, count_ms, nbytes
+    achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
+    pipe_gbs = (nbytes + b_out) / ((count_ms + fill_ms) * 1e-3) / 1e9
+    line = {
+        "metric": "device-resident libsvm parse GB/s (input bytes) at 1/2/4/8 GPU; % HBM roofline",
+        "value": round(value, 3),
+        "unit": "GB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (tools/synth.c splitmix64 seed 1, %%.9g values), HBM-resident",
+        "config": {"workload": DESC[args.config], "baseline_config": cfg_idx, "format": fmt,
+                   "rows_per_gpu": rows, "width": width, "input_bytes_per_gpu": nbytes,
+                   "csr_bytes_per_gpu": b_out, "nnz_per_gpu": int(counts[dmlc_amd.INDEX]),
+                   "chunks_per_gpu": len(starts) - 1, "parallelism": "shard%d" % world},
+        "hbm_frac_input": round(value / world / HBM_PEAK_GBS, 4),
+        "hbm_frac_in_out": round((total_in + b_out * world) * args.steps / elapsed / 1e9
+                                 / world / HBM_PEAK_GBS, 4),
+        "phase_ms": {"count": round(count_ms, 4), "fill": round(fill_ms, 4)},
+        "pipeline_in_out_GBs": round(pipe_gbs, 2),
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "bytes_per_launch": dom_bytes, "avg_ms": round(dom_ms, 4)},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            line["cpu_baseline"] = cpu_baseline(text, starts, fmt, args.cpu_budget)
+        except Exception as e:  # reported, never fatal for the GPU number
+            line["cpu_baseline"] = {"error": repr(e)}
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -101,6 +101,10 @@ int dmlc_amd_parse(const void *d_text, uint64_t nbytes, const uint64_t *d_chunk_
   if (!tile_cnt || !tile_base || !chunk_min || !chunk_sink) return DMLC_AMD_ERR_ARG;
   uint64_t *res = reinterpret_cast<uint64_t *>(d_result);
   const bool count_only = (prm->flags & DMLC_AMD_FLAG_COUNT_ONLY) != 0;
+  const bool fill_only = (prm->flags & DMLC_AMD_FLAG_FILL_ONLY) != 0;
+  if (count_only && fill_only) return DMLC_AMD_ERR_ARG;
+  const int phase = count_only ? dmlc_amd::kPhaseCount
+                               : (fill_only ? dmlc_amd::kPhaseFill : dmlc_amd::kPhaseFull);
   hipError_t e = hipSuccess;
   if (prm->format == DMLC_AMD_LIBSVM) {
     dmlc_amd::LibsvmArgs a;
@@ -125,7 +129,7 @@ int dmlc_amd_parse(const void *d_text, uint64_t nbytes, const uint64_t *d_chunk_
     a.chunk_tab = d_chunk_table ? d_chunk_table : chunk_sink;
     a.chunk_min = chunk_min;
     a.err = reinterpret_cast<unsigned long long *>(res + 8);
-    e = dmlc_amd::launch_libsvm(a, res, count_only, s);
+    e = dmlc_amd::launch_libsvm(a, res, phase, s);
   } else if (prm->format == DMLC_AMD_CSV) {
     dmlc_amd::CsvArgs a;
     std::memset(&a, 0, sizeof(a));
@@ -151,7 +155,7 @@ int dmlc_amd_parse(const void *d_text, uint64_t nbytes, const uint64_t *d_chunk_
     for (int i = 0; i < 8; ++i) a.cap[i] = out->cap[i];
     a.chunk_tab = d_chunk_table ? d_chunk_table : chunk_sink;
     a.err = reinterpret_cast<unsigned long long *>(res + 8);
-    e = dmlc_amd::launch_csv(a, res, count_only, s);
+    e = dmlc_amd::launch_csv(a, res, phase, s);
   } else {
     return DMLC_AMD_ERR_ARG;  // libfm: not built yet
   }

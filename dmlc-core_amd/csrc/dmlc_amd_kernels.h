@@ -8,9 +8,13 @@
 
 namespace dmlc_amd {
 
-// Launch count -> scan -> write on `s`.  `res` is the device result block
-// (dmlc_amd_result layout).  count_only skips the write pass.
-hipError_t launch_libsvm(const LibsvmArgs &a, uint64_t *res, bool count_only, hipStream_t s);
-hipError_t launch_csv(const CsvArgs &a, uint64_t *res, bool count_only, hipStream_t s);
+// Pipeline phases: full = count -> scan -> write; count = count -> scan (the
+// size query; tile bases stay in the workspace); fill = write only, reusing
+// the tile bases a count phase left in the same workspace.
+enum { kPhaseFull = 0, kPhaseCount = 1, kPhaseFill = 2 };
+
+// Launch the phase on `s`.  `res` is the device result block (dmlc_amd_result layout).
+hipError_t launch_libsvm(const LibsvmArgs &a, uint64_t *res, int phase, hipStream_t s);
+hipError_t launch_csv(const CsvArgs &a, uint64_t *res, int phase, hipStream_t s);
 
 }  // namespace dmlc_amd

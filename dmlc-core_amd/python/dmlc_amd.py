@@ -17,6 +17,7 @@ LIBSVM, CSV, LIBFM = 0, 1, 2
 F32, I32, I64 = 0, 1, 2
 ROWS, INDEX, VALUE, WEIGHT, QID, LABEL, FIELD = range(7)
 FLAG_COUNT_ONLY = 1
+FLAG_FILL_ONLY = 2
 ERR_CAPACITY = 16
 _FMT = {"libsvm": LIBSVM, "csv": CSV, "libfm": LIBFM}
 _VT = {"f32": F32, "float32": F32, "i32": I32, "int32": I32, "i64": I64, "int64": I64}
@@ -126,14 +127,29 @@ class DeviceParser:
         if rc != 0:
             raise RuntimeError("dmlc_amd_parse: %s" % lib().dmlc_amd_error_string(rc).decode())
 
-    def count(self, text, chunk_starts, stream=None):
-        """Size query: exact per-slot totals (device work, then a host sync)."""
+    def count(self, text, chunk_starts, stream=None, result=None):
+        """Size query: exact per-slot totals (device work, then a host sync).
+        The per-tile counts stay in this parser's workspace for fill()."""
         torch = self.torch
-        res = torch.zeros(16, dtype=torch.int64, device="cuda")
+        res = result if result is not None else torch.zeros(16, dtype=torch.int64, device="cuda")
+        self.count_async(text, chunk_starts, res, stream=stream)
+        if stream is not None:
+            stream.synchronize()
+        return res.cpu().numpy().view(np.uint64)
+
+    def count_async(self, text, chunk_starts, result, out=None, stream=None):
+        """Launch the count phase (count -> scan) without a host sync."""
         p = Params.from_buffer_copy(self.params)
         p.flags |= FLAG_COUNT_ONLY
-        self._call(text, chunk_starts, Csr(), None, res, p, stream)
-        return res.cpu().numpy().view(np.uint64)
+        csr = Csr() if out is None else out.get("_csr") or self.csr_of(out)
+        self._call(text, chunk_starts, csr, None, result, p, stream)
+
+    def fill_async(self, text, chunk_starts, out, result, chunk_table=None, stream=None):
+        """Launch the write pass over the counts of the preceding count phase."""
+        p = Params.from_buffer_copy(self.params)
+        p.flags |= FLAG_FILL_ONLY
+        self._call(text, chunk_starts, out.get("_csr") or self.csr_of(out), chunk_table, result, p,
+                   stream)
 
     def alloc(self, counts):
         """Allocate exact-size outputs for the given totals."""
@@ -170,14 +186,14 @@ class DeviceParser:
                    chunk_table, result, self.params, stream)
 
     def parse(self, text, chunk_starts, stream=None):
-        """Count, allocate, parse; returns dict of device tensors + counts/error."""
+        """Count, allocate, fill; returns dict of device tensors + counts/error."""
         torch = self.torch
-        counts = self.count(text, chunk_starts, stream)
+        res = torch.zeros(16, dtype=torch.int64, device="cuda")
+        counts = self.count(text, chunk_starts, stream, result=res)
         out = self.alloc(counts)
         nchunks = int(chunk_starts.numel()) - 1
         out["chunk_table"] = torch.zeros(max(nchunks, 1) * 8, dtype=torch.int64, device="cuda")
-        res = torch.zeros(16, dtype=torch.int64, device="cuda")
-        self.parse_into(text, chunk_starts, out, res,
+        self.fill_async(text, chunk_starts, out, res,
                         chunk_table=out["chunk_table"] if nchunks > 0 else None, stream=stream)
         r = res.cpu().numpy().view(np.uint64)
         out["error"] = int(r[8])
@@ -276,3 +292,37 @@ def chunk_check(h, fmt, nchunks, total_counts):
         if rows and not (val == 0 or val == idx):
             return c
     return -1
+
+
+def text_chunk_starts(text, chunk_bytes=8 << 20):
+    """Chunk boundaries an InputSplit ("text", one part) would hand over for
+    this buffer: each chunk ends just after the last '\\n' / '\\r' inside its
+    `chunk_bytes` read buffer (LineSplitter::FindLastRecordBegin,
+    src/io/line_split.cc:37-45; kBufferSize, src/io/input_split_base.h:39); a
+    record longer than the buffer grows it until one fits
+    (input_split_base.cc:272-291).  Returns int64 [nchunks + 1] offsets."""
+    a = np.frombuffer(text, dtype=np.uint8) if not isinstance(text, np.ndarray) else text
+    n = int(a.size)
+    if n == 0:
+        return np.zeros(1, dtype=np.int64)
+    nl = np.flatnonzero((a == 10) | (a == 13)) + 1  # candidate chunk ends (record begins)
+    starts = [0]
+    s = 0
+    while s < n:
+        lim = s + chunk_bytes
+        if lim >= n:
+            starts.append(n)
+            break
+        while True:
+            # last newline at p with s < p < lim; the record begins at p + 1
+            j = int(np.searchsorted(nl, lim, side="right")) - 1
+            if j >= 0 and int(nl[j]) - 1 > s:
+                e = int(nl[j])
+                break
+            lim = s + (lim - s) * 2  # record longer than the buffer: grow
+            if lim >= n:
+                e = n
+                break
+        starts.append(e)
+        s = e
+    return np.asarray(starts, dtype=np.int64)

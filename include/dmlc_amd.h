@@ -78,6 +78,11 @@ typedef struct dmlc_amd_params {
 } dmlc_amd_params;
 
 #define DMLC_AMD_FLAG_COUNT_ONLY 1u /* run the counting passes only (size query) */
+/* Run the write pass only, reusing the per-tile counts that a COUNT_ONLY call
+ * on the same text, chunk starts, params and workspace left behind (earlier on
+ * the same stream).  COUNT_ONLY then FILL_ONLY does exactly the work of one
+ * full call, with a host-side allocation in between. */
+#define DMLC_AMD_FLAG_FILL_ONLY 2u
 
 typedef struct dmlc_amd_csr {
   uint64_t *offset; /* rows + 1 (global, rebased across chunks) */

@@ -1,3 +1,4 @@
+#define _POSIX_C_SOURCE 199309L
 /*
  * dmlc_oracle.c -- TEST INFRASTRUCTURE ONLY (see dmlc_oracle.h).
  *
@@ -16,6 +17,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 /* ---------------------------------------------------------------- bytes -- */
 
@@ -849,4 +851,23 @@ void dmo_chunks_free(dmo_chunks *c) {
   free(c->off);
   free(c->buf);
   memset(c, 0, sizeof(*c));
+}
+
+/* ---------------------------------------------------------------- bench -- */
+
+double dmo_bench_chunks(const char *buf, const uint64_t *off, int nchunks, const dmo_params *prm,
+                        uint64_t *nnz) {
+  struct timespec t0, t1;
+  uint64_t total = 0;
+  clock_gettime(CLOCK_MONOTONIC, &t0);
+  for (int i = 0; i < nchunks; ++i) {
+    dmo_csr c;
+    dmo_csr_init(&c, prm->value_kind);
+    dmo_parse_chunk(buf + off[i], (size_t)(off[i + 1] - off[i]), prm, &c);
+    total += c.n_index;
+    dmo_csr_free(&c);
+  }
+  clock_gettime(CLOCK_MONOTONIC, &t1);
+  if (nnz) *nnz = total;
+  return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
 }

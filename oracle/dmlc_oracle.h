@@ -86,6 +86,13 @@ int dmo_split_text(const char *const *files, const uint64_t *sizes, int nfiles,
                    unsigned rank, unsigned nsplit, uint64_t buffer_bytes, dmo_chunks *out);
 void dmo_chunks_free(dmo_chunks *c);
 
+/* Timing helper for bench.py's cpu_baseline leg: parse chunk i = buf[off[i] ..
+ * off[i+1]) for every i on the calling thread (fresh output per chunk, as the
+ * reference reuses one container per chunk); returns seconds, *nnz = total
+ * index count. */
+double dmo_bench_chunks(const char *buf, const uint64_t *off, int nchunks, const dmo_params *prm,
+                        uint64_t *nnz);
+
 #ifdef __cplusplus
 }
 #endif

@@ -101,6 +101,9 @@ def oracle_lib():
                                      ctypes.c_int, ctypes.c_uint, ctypes.c_uint, ctypes.c_uint64,
                                      ctypes.POINTER(Chunks)]
         L.dmo_chunks_free.argtypes = [ctypes.POINTER(Chunks)]
+        L.dmo_bench_chunks.restype = ctypes.c_double
+        L.dmo_bench_chunks.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                       ctypes.POINTER(Params), ctypes.POINTER(ctypes.c_uint64)]
         _ORACLE = L
     return _ORACLE
 
@@ -209,6 +212,28 @@ def split_text(files, rank=0, nsplit=1, buffer_bytes=8 << 20):
     data = _arr(c.buf, int(off[-1]), np.uint8).tobytes() if c.n_chunks else b""
     oracle_lib().dmo_chunks_free(ctypes.byref(c))
     return [data[int(a):int(b)] for a, b in zip(off[:-1], off[1:])]
+
+
+def bench_chunks(buf, offs, fmt=LIBSVM, nthread=1, use_ref=None):
+    """CPU-baseline timing (bench.py only): parse the chunks buf[offs[i]:offs[i+1]].
+
+    Uses the genuine reference's ParseBlock (oracle/_ref, ``nthread`` threads
+    each taking whole chunks) when it is built, else the C restatement on one
+    thread.  Returns (seconds, nnz, kind, threads)."""
+    buf = np.ascontiguousarray(buf, dtype=np.uint8)
+    offs = np.ascontiguousarray(offs, dtype=np.uint64)
+    nch = len(offs) - 1
+    nnz = ctypes.c_uint64(0)
+    if use_ref is None:
+        use_ref = ref_available()
+    if use_ref:
+        secs = ref_lib().ref_bench_blocks(buf.ctypes.data, offs.ctypes.data, nch, fmt, nthread,
+                                          ctypes.byref(nnz))
+        return secs, int(nnz.value), "reference", nthread
+    prm = params(fmt=fmt)
+    secs = oracle_lib().dmo_bench_chunks(buf.ctypes.data, offs.ctypes.data, nch, ctypes.byref(prm),
+                                         ctypes.byref(nnz))
+    return secs, int(nnz.value), "port", 1
 
 
 # ------------------------------------------------------------------ reference

@@ -12,13 +12,19 @@ EXE = os.path.join(HERE, "_build", "emu_asan")
 _FMT = {"libsvm": 0, "csv": 1, "libfm": 2}
 
 
+_BUILT = False
+
+
 def build():
+    """(Re)build the emulator when its sources changed (make is a no-op otherwise)."""
+    global _BUILT
     subprocess.check_call(["make", "-s", "-C", HERE])
+    _BUILT = True
 
 
 def parse(data, chunk_offsets=None, fmt="libsvm", index_bits=32, value_type=0, indexing_mode=0,
           label_column=-1, weight_column=-1, delimiter=",", tile_bytes=0):
-    if not os.path.exists(EXE):
+    if not _BUILT:
         build()
     raw = data.encode("latin-1") if isinstance(data, str) else bytes(data)
     if chunk_offsets is None:
