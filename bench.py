@@ -78,8 +78,7 @@ def cpu_baseline(text, starts, fmt, budget_s):
     return {"value": round(nb / secs / 1e9, 4), "unit": "GB/s", "cores": thr, "kind": kind,
             "sample": "%d of %d InputSplit chunks (%.1f MB, %d nnz) of the same shard, "
                       "ParseBlock per chunk, %d thread(s) (reference cap min(max(nproc/2-4,1),2), "
-                      "nproc=%d), %.1f s" % (k, len(starts) - 1, nb / 1e6, nnz, thr, thr, nproc,
-                                             secs)}
+                      "nproc=%d), %.1f s" % (k, len(starts) - 1, nb / 1e6, nnz, thr, nproc, secs)}
 
 
 def main():
@@ -194,7 +193,7 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic (tools/synth.c splitmix64 seed 1, %%.9g values), HBM-resident",
+        "data": "synthetic (tools/synth.c splitmix64 seed 1, %.9g values), HBM-resident",
         "config": {"workload": DESC[args.config], "baseline_config": cfg_idx, "format": fmt,
                    "rows_per_gpu": rows, "width": width, "input_bytes_per_gpu": nbytes,
                    "csr_bytes_per_gpu": b_out, "nnz_per_gpu": int(counts[dmlc_amd.INDEX]),

@@ -23,7 +23,7 @@ struct DevBlock {
     return o;
   }
 
-  __device__ uint64_t min_u64(uint64_t v) const {
+  __device__ __forceinline__ uint64_t min_u64(uint64_t v) const {
     const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) {
@@ -41,7 +41,7 @@ struct DevBlock {
 
   // Exclusive prefix (identity for thread 0) and the block total.
   template <typename T, typename Op>
-  __device__ T exclusive(T v, T identity, Op op, T *total) const {
+  __device__ __forceinline__ T exclusive(T v, T identity, Op op, T *total) const {
     static_assert(sizeof(T) <= 64, "scan element too large");
     T *sc = reinterpret_cast<T *>(scratch);
     const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;

@@ -6,7 +6,7 @@
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
 #define DA_HD __host__ __device__ __forceinline__
-#define DA_HDF __host__ __device__
+#define DA_HDF __host__ __device__ __forceinline__
 #else
 #include <cstring>
 #define DA_HD inline
