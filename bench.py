@@ -130,15 +130,11 @@ def main():
     b_out = csr_bytes(counts)
     s = torch.cuda.current_stream()
 
-    def step(evs=None):
-        if evs:
-            evs[0].record(s)
-        p.count_async(d_text, d_starts, res, out=out)
-        if evs:
-            evs[1].record(s)
-        p.fill_async(d_text, d_starts, out, res)
-        if evs:
-            evs[2].record(s)
+    def step():
+        # one full dmlc_amd_parse call (flags 0) into pre-allocated outputs: the
+        # single-pass kernel when the text is in the uniform grammar, else the
+        # exact count -> scan -> write pipeline
+        p.parse_into(d_text, d_starts, out, res)
 
     for _ in range(args.warmup):
         step()
@@ -147,25 +143,25 @@ def main():
     if int(r[8]) != 0:
         raise RuntimeError("parse error %#x" % int(r[8]))
     if [int(x) for x in r[:7]] != [int(x) for x in counts[:7]]:
-        raise RuntimeError("count mismatch between phases")
+        raise RuntimeError("count mismatch between calls")
+    path = "exact tile kernels" if int(r[9]) else "single-pass uniform-grammar kernel"
 
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
+    dmlc_amd.profile_begin()
     t_start = time.perf_counter()
-    for k in range(args.steps):
-        step(evs[k])
+    for _ in range(args.steps):
+        step()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
+    kern_ms, launches, kern_name = dmlc_amd.profile_end()
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    count_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
-    fill_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
     r = res.cpu().numpy().view(np.uint64)
     if int(r[8]) != 0:
         raise RuntimeError("parse error %#x" % int(r[8]))
@@ -173,14 +169,10 @@ def main():
     ms_per_step = elapsed * 1e3 / args.steps
     total_in = nbytes * world
     value = total_in * args.steps / elapsed / 1e9
-    # dominant kernel: the write pass reads the text and writes the CSR (B_in + B_out);
-    # the count pass reads the text (B_in)
-    if fill_ms >= count_ms:
-        dom, dom_ms, dom_bytes = "%s_tile<2> (write pass)" % fmt, fill_ms, nbytes + b_out
-    else:
-        dom, dom_ms, dom_bytes = "%s_tile<1> (count pass)" % fmt, count_ms, nbytes
+    # dominant kernel: reads the text once and writes the CSR once (B_in + B_out)
+    dom_ms = kern_ms / max(launches, 1)
+    dom_bytes = nbytes + b_out
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
-    pipe_gbs = (nbytes + b_out) / ((count_ms + fill_ms) * 1e-3) / 1e9
     line = {
         "metric": "device-resident libsvm parse GB/s (input bytes) at 1/2/4/8 GPU; % HBM roofline",
         "value": round(value, 3),
@@ -201,9 +193,8 @@ def main():
         "hbm_frac_input": round(value / world / HBM_PEAK_GBS, 4),
         "hbm_frac_in_out": round((total_in + b_out * world) * args.steps / elapsed / 1e9
                                  / world / HBM_PEAK_GBS, 4),
-        "phase_ms": {"count": round(count_ms, 4), "fill": round(fill_ms, 4)},
-        "pipeline_in_out_GBs": round(pipe_gbs, 2),
-        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2),
+        "path": path,
+        "roofline": {"bound": "hbm", "kernel": kern_name, "achieved": round(achieved, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                      "bytes_per_launch": dom_bytes, "avg_ms": round(dom_ms, 4)},

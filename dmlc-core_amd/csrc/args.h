@@ -26,6 +26,31 @@ struct LibsvmArgs {
   uint64_t *chunk_tab;  // [nchunk][C_N] exclusive counts at each chunk start (may be a sink)
   uint64_t *chunk_min;  // [nchunk] min index per chunk (indexing_mode < 0)
   unsigned long long *err;
+  const uint32_t *gate;  // when set, the tile kernels run only if *gate != 0
+};
+
+// Single-pass uniform-grammar libsvm kernel (svm_fast.h).
+struct FastSvmArgs {
+  const uint8_t *text;
+  uint64_t n;
+  const uint64_t *cs;
+  int nchunk;
+  uint32_t ntiles;
+  int wide;
+  int indexing_mode;
+  int skip_if_gated;  // fill phase: do nothing when the count phase fell back
+  uint64_t *offset;
+  float *label;
+  float *weight;
+  void *index;
+  float *value;
+  uint64_t cap[8];
+  uint64_t *chunk_tab;  // may be null
+  uint64_t *lb;         // [ntiles][4] look-back words, zeroed per launch
+  uint32_t *ticket;     // tile ticket counter, zeroed per launch
+  uint32_t *gate;       // != 0: input left the grammar -> exact path
+  unsigned long long *err;  // first error of this path
+  uint64_t *res;        // dmlc_amd_result counts (written by the last tile)
 };
 
 struct CsvArgs {

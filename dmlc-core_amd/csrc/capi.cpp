@@ -2,13 +2,15 @@
 #include <hip/hip_runtime.h>
 
 #include <cstring>
+#include <vector>
 
 #include "dmlc_amd.h"
 #include "dmlc_amd_kernels.h"
 
 namespace {
 
-constexpr uint64_t kDefaultTile = 256ull << 10;  // bytes of text owned per workgroup
+constexpr uint64_t kDefaultTile = 256ull << 10;  // bytes of text owned per workgroup (exact kernels)
+constexpr uint64_t kFastTile = 16ull << 10;      // svm_fast.h kTile
 constexpr int kSlots = 7;
 
 uint64_t tile_of(const dmlc_amd_params *p) {
@@ -42,9 +44,64 @@ bool csv_delim_fast(int d, int vtype) {
   return true;
 }
 
+// ---- kernel timing (dmlc_amd_profile_begin / _end)
+struct Profile {
+  bool on = false;
+  std::vector<hipEvent_t> ev;  // pairs: begin, end
+  size_t used = 0;
+  const char *kernel = "";
+};
+thread_local Profile g_prof;
+
 }  // namespace
 
+namespace dmlc_amd {
+void prof_mark(int end, hipStream_t s, const char *kernel) {
+  Profile &p = g_prof;
+  if (!p.on) return;
+  if (!end) {
+    if (p.used + 2 > p.ev.size()) {
+      for (int i = 0; i < 64; ++i) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return;
+        p.ev.push_back(e);
+      }
+    }
+    hipEventRecord(p.ev[p.used], s);
+    p.kernel = kernel;
+  } else {
+    hipEventRecord(p.ev[p.used + 1], s);
+    p.used += 2;
+  }
+}
+}  // namespace dmlc_amd
+
 extern "C" {
+
+int dmlc_amd_profile_begin(void) {
+  g_prof.on = true;
+  g_prof.used = 0;
+  return DMLC_AMD_OK;
+}
+
+int dmlc_amd_profile_end(double *total_ms, int *launches, const char **kernel) {
+  Profile &p = g_prof;
+  p.on = false;
+  double t = 0;
+  for (size_t i = 0; i + 1 < p.used; i += 2) {
+    float ms = 0;
+    if (hipEventSynchronize(p.ev[i + 1]) != hipSuccess ||
+        hipEventElapsedTime(&ms, p.ev[i], p.ev[i + 1]) != hipSuccess)
+      return DMLC_AMD_ERR_HIP;
+    t += ms;
+  }
+  if (total_ms) *total_ms = t;
+  if (launches) *launches = (int)(p.used / 2);
+  if (kernel) *kernel = p.kernel;
+  p.used = 0;
+  return DMLC_AMD_OK;
+}
+
 
 int dmlc_amd_abi_version(void) { return DMLC_AMD_ABI_VERSION; }
 
@@ -71,7 +128,8 @@ size_t dmlc_amd_workspace_bytes(uint64_t nbytes, int nchunks, const dmlc_amd_par
   const uint64_t T = tile_of(prm);
   const uint64_t ntiles = (nbytes + T - 1) / T;
   const uint64_t nc = nchunks > 0 ? (uint64_t)nchunks : 1;
-  return (size_t)((2 * ntiles * kSlots + nc + nc * 8) * sizeof(uint64_t) + 8 * 256);
+  const uint64_t nft = (nbytes + kFastTile - 1) / kFastTile;
+  return (size_t)((2 * ntiles * kSlots + nc + nc * 8 + nft * 4) * sizeof(uint64_t) + 11 * 256);
 }
 
 int dmlc_amd_parse(const void *d_text, uint64_t nbytes, const uint64_t *d_chunk_starts, int nchunks,
@@ -98,7 +156,11 @@ int dmlc_amd_parse(const void *d_text, uint64_t nbytes, const uint64_t *d_chunk_
   uint64_t *tile_base = cv.take<uint64_t>(ntiles * kSlots + 1);
   uint64_t *chunk_min = cv.take<uint64_t>(nc);
   uint64_t *chunk_sink = cv.take<uint64_t>((size_t)nc * 8);
-  if (!tile_cnt || !tile_base || !chunk_min || !chunk_sink) return DMLC_AMD_ERR_ARG;
+  const uint64_t nft = (nbytes + kFastTile - 1) / kFastTile;
+  uint32_t *ctl = cv.take<uint32_t>(4);               // gate, ticket
+  unsigned long long *ferr = cv.take<unsigned long long>(1);
+  uint64_t *lb = cv.take<uint64_t>(nft * 4 + 1);
+  if (!tile_cnt || !tile_base || !chunk_min || !chunk_sink || !ctl || !ferr || !lb) return DMLC_AMD_ERR_ARG;
   uint64_t *res = reinterpret_cast<uint64_t *>(d_result);
   const bool count_only = (prm->flags & DMLC_AMD_FLAG_COUNT_ONLY) != 0;
   const bool fill_only = (prm->flags & DMLC_AMD_FLAG_FILL_ONLY) != 0;
@@ -129,7 +191,31 @@ int dmlc_amd_parse(const void *d_text, uint64_t nbytes, const uint64_t *d_chunk_
     a.chunk_tab = d_chunk_table ? d_chunk_table : chunk_sink;
     a.chunk_min = chunk_min;
     a.err = reinterpret_cast<unsigned long long *>(res + 8);
-    e = dmlc_amd::launch_libsvm(a, res, phase, s);
+    a.gate = ctl;
+    dmlc_amd::FastSvmArgs f;
+    std::memset(&f, 0, sizeof(f));
+    f.text = a.text;
+    f.n = nbytes;
+    f.cs = d_chunk_starts;
+    f.nchunk = nchunks;
+    f.ntiles = (uint32_t)nft;
+    f.wide = a.wide;
+    f.indexing_mode = prm->indexing_mode;
+    f.skip_if_gated = phase == dmlc_amd::kPhaseFill;
+    f.offset = a.offset;
+    f.label = a.label;
+    f.weight = a.weight;
+    f.index = a.index;
+    f.value = a.value;
+    for (int i = 0; i < 8; ++i) f.cap[i] = out->cap[i];
+    f.chunk_tab = d_chunk_table;
+    f.lb = lb;
+    f.ticket = ctl + 1;
+    f.gate = ctl;
+    f.err = ferr;
+    f.res = res;
+    const bool use_fast = nbytes > 0 && prm->indexing_mode >= 0 && !(prm->flags & DMLC_AMD_FLAG_EXACT);
+    e = dmlc_amd::launch_libsvm(a, f, use_fast, res, phase, s);
   } else if (prm->format == DMLC_AMD_CSV) {
     dmlc_amd::CsvArgs a;
     std::memset(&a, 0, sizeof(a));

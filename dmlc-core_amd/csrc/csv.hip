@@ -27,6 +27,7 @@ __global__ void reopen_kernel(uint64_t *res, uint64_t *offset, uint64_t cap_rows
 
 __global__ void finalize_kernel(uint64_t *res) {
   if (res[8] == ~0ull) res[8] = 0;
+  res[9] = 1;  // dmlc_amd_result.path: exact tile kernels
 }
 
 }  // namespace
@@ -45,9 +46,13 @@ hipError_t launch_csv(const CsvArgs &a, uint64_t *res, int phase, hipStream_t s)
     if (phase != kPhaseFill) {
       csv_tile<1><<<a.ntiles, kThreads, 0, s>>>(a);
       tile_scan_kernel<<<1, kThreads, 0, s>>>(a.tile_cnt, const_cast<uint64_t *>(a.tile_base), a.ntiles,
-                                              res, a.offset, a.cap[C_ROWS]);
+                                              res, a.offset, a.cap[C_ROWS], nullptr);
     }
-    if (phase != kPhaseCount) csv_tile<2><<<a.ntiles, kThreads, 0, s>>>(a);
+    if (phase != kPhaseCount) {
+      prof_mark(0, s, "csv_tile<2>");
+      csv_tile<2><<<a.ntiles, kThreads, 0, s>>>(a);
+      prof_mark(1, s, "csv_tile<2>");
+    }
   }
   finalize_kernel<<<1, 1, 0, s>>>(res);
   return hipGetLastError();

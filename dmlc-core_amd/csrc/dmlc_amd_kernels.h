@@ -13,8 +13,16 @@ namespace dmlc_amd {
 // the tile bases a count phase left in the same workspace.
 enum { kPhaseFull = 0, kPhaseCount = 1, kPhaseFill = 2 };
 
+// Kernel timing hook (capi.cpp): launchers bracket their dominant kernel with
+// prof_mark(0, ...) / prof_mark(1, ...); a no-op unless dmlc_amd_profile_begin
+// was called on this thread.
+void prof_mark(int end, hipStream_t s, const char *kernel);
+
 // Launch the phase on `s`.  `res` is the device result block (dmlc_amd_result layout).
-hipError_t launch_libsvm(const LibsvmArgs &a, uint64_t *res, int phase, hipStream_t s);
+// libsvm: the uniform-grammar kernel (f) runs first when use_fast; the exact
+// kernels (a) run when it sets the gate word (f.gate), or always when !use_fast.
+hipError_t launch_libsvm(const LibsvmArgs &a, const FastSvmArgs &f, bool use_fast, uint64_t *res,
+                         int phase, hipStream_t s);
 hipError_t launch_csv(const CsvArgs &a, uint64_t *res, int phase, hipStream_t s);
 
 }  // namespace dmlc_amd

@@ -43,6 +43,61 @@ DA_HD void atomic_min_u64(unsigned long long *p, unsigned long long v) {
 #endif
 }
 
+DA_HD uint32_t atomic_add_u32(uint32_t *p, uint32_t v) {  // returns the old value
+#if defined(__HIP_DEVICE_COMPILE__)
+  return atomicAdd(p, v);
+#else
+  return __atomic_fetch_add(p, v, __ATOMIC_RELAXED);
+#endif
+}
+
+// Look-back words: one 8-byte {status, value} word per counter, stored and
+// polled whole by agent-scope relaxed atomics (sc1: no L1, no tearing), so no
+// fence or separate flag is needed (MI355X_MICROARCH.md, visibility: R2 form).
+DA_HD void store_agent_u64(uint64_t *p, uint64_t v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+  __atomic_store_n(p, v, __ATOMIC_RELEASE);
+#endif
+}
+DA_HD uint64_t load_agent_u64(uint64_t *p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+  return __atomic_load_n(p, __ATOMIC_ACQUIRE);
+#endif
+}
+DA_HD void spin_pause() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_s_sleep(2);
+#endif
+}
+
+// v_perm_b32: byte i of the result = byte sel[i] (0..7) of {s0:s1} (s1 = bytes 0-3).
+// Callers only pass selectors 0..7.
+DA_HD uint32_t perm_b32(uint32_t s0, uint32_t s1, uint32_t sel) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_perm(s0, s1, sel);
+#else
+  const uint64_t src = ((uint64_t)s0 << 32) | s1;
+  uint32_t r = 0;
+  for (int i = 0; i < 4; ++i) r |= (uint32_t)((src >> (8 * ((sel >> (8 * i)) & 7))) & 0xFF) << (8 * i);
+  return r;
+#endif
+}
+
+DA_HD int popc64(uint64_t x) { return __builtin_popcountll(x); }
+DA_HD int ctz64(uint64_t x) { return __builtin_ctzll(x); }
+DA_HD int clz64(uint64_t x) { return __builtin_clzll(x); }
+// x + y + cin, returning the carry out of bit 63
+DA_HD uint64_t add_carry(uint64_t x, uint64_t y, uint32_t cin, uint32_t *cout) {
+  const uint64_t s = x + y;
+  const uint64_t r = s + cin;
+  *cout = (uint32_t)((s < x) | (r < s));
+  return r;
+}
+
 template <typename T>
 DA_HD T mn(T a, T b) { return a < b ? a : b; }
 template <typename T>

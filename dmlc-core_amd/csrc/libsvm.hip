@@ -1,9 +1,15 @@
-// libsvm.hip -- MI355X kernels for LibSVMParser::ParseBlock (libsvm_parser.h:85-172);
-// the tile body lives in libsvm_core.h.
+// libsvm.hip -- MI355X kernels for LibSVMParser::ParseBlock (libsvm_parser.h:85-172).
+//
+//   svm_fast_tile   single-pass uniform-grammar kernel (svm_fast.h): the
+//                   normal path; sets the gate word when the input leaves
+//                   the grammar
+//   libsvm_tile     exact count / write tile kernels (libsvm_core.h), run
+//                   only when the gate is set (or indexing_mode < 0)
 #include "block.h"
 #include "dmlc_amd_kernels.h"
 #include "libsvm_core.h"
 #include "scan.h"
+#include "svm_fast.h"
 
 namespace dmlc_amd {
 namespace {
@@ -16,31 +22,68 @@ __global__ void __launch_bounds__(kThreads) libsvm_tile(LibsvmArgs a) {
   svm::tile<MODE>(a, sh, bk, blockIdx.x);
 }
 
-// fill phase after a count phase: the count phase's finalize turned "no error"
-// (~0) into 0; reopen it so the write pass can record the first error, and
-// store the closing offset (the reference's final push, libsvm_parser.h:157-159)
-// the size query could not (it had no output buffers)
-__global__ void reopen_kernel(uint64_t *res, uint64_t *offset, uint64_t cap_rows) {
+template <int MODE>
+__global__ void __launch_bounds__(kThreads) svm_fast_tile(FastSvmArgs a) {
+  __shared__ __attribute__((aligned(16))) fsvm::Shared sh;
+  __shared__ uint64_t scratch[kBlockScratchU64];
+  DevBlock bk{scratch};
+  fsvm::tile<MODE>(a, sh, bk);
+}
+
+// fill phase after a count phase that fell back to the exact kernels: the
+// count phase's select turned "no error" (~0) into 0; reopen it so the write
+// pass can record the first error, and store the closing offset (the
+// reference's final push, libsvm_parser.h:157-159) the size query could not
+__global__ void reopen_kernel(uint64_t *res, uint64_t *offset, uint64_t cap_rows, const uint32_t *gate) {
+  if (*gate == 0) return;
   if (res[8] == 0) res[8] = ~0ull;
   if (offset && res[0] < cap_rows + 1) offset[res[0]] = res[1];
 }
 
-__global__ void finalize_kernel(uint64_t *res) {
-  if (res[8] == ~0ull) res[8] = 0;  // no error raised
+// the error of whichever path produced the result
+__global__ void select_kernel(uint64_t *res, const uint32_t *gate, const unsigned long long *ferr) {
+  if (*gate == 0) res[8] = *ferr;
+  if (res[8] == ~0ull) res[8] = 0;
+  res[9] = *gate;  // dmlc_amd_result.path
 }
 
 }  // namespace
 
-hipError_t launch_libsvm(const LibsvmArgs &a, uint64_t *res, int phase, hipStream_t s) {
+hipError_t launch_libsvm(const LibsvmArgs &a, const FastSvmArgs &f, bool use_fast, uint64_t *res,
+                         int phase, hipStream_t s) {
   hipError_t e;
+  uint32_t *gate = f.gate;
   if (phase != kPhaseFill) {
     if ((e = hipMemsetAsync(res, 0, 16 * sizeof(uint64_t), s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(res + 8, 0xFF, sizeof(uint64_t), s)) != hipSuccess) return e;
+    // gate = 0 (fast path decides) or 1 (exact path only)
+    if ((e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(gate), use_fast ? 0 : 1, 1, s)) !=
+        hipSuccess)
+      return e;
+  }
+  if (use_fast) {
+    if ((e = hipMemsetAsync(f.ticket, 0, sizeof(uint32_t), s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(f.err, 0xFF, sizeof(uint64_t), s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(f.lb, 0, (size_t)f.ntiles * 4 * sizeof(uint64_t), s)) != hipSuccess) return e;
+    if (phase == kPhaseCount) {
+      prof_mark(0, s, "svm_fast_tile<1>");
+      svm_fast_tile<1><<<f.ntiles, kThreads, 0, s>>>(f);
+      prof_mark(1, s, "svm_fast_tile<1>");
+    } else {
+      prof_mark(0, s, "svm_fast_tile<2>");
+      svm_fast_tile<2><<<f.ntiles, kThreads, 0, s>>>(f);
+      prof_mark(1, s, "svm_fast_tile<2>");
+    }
+  } else if ((e = hipMemsetAsync(f.err, 0xFF, sizeof(uint64_t), s)) != hipSuccess) {
+    return e;
+  }
+  // ---- exact path, gated on the device flag (early exit when the fast path stood)
+  if (phase != kPhaseFill) {
     if (a.indexing_mode < 0 &&
         (e = hipMemsetAsync(a.chunk_min, 0xFF, (size_t)a.nchunk * sizeof(uint64_t), s)) != hipSuccess)
       return e;
   } else {
-    reopen_kernel<<<1, 1, 0, s>>>(res, a.offset, a.cap[C_ROWS]);
+    reopen_kernel<<<1, 1, 0, s>>>(res, a.offset, a.cap[C_ROWS], gate);
   }
   if (!a.ntiles && phase != kPhaseCount && a.offset && (e = hipMemsetAsync(a.offset, 0, 8, s)) != hipSuccess)
     return e;  // empty input: offset = {0}
@@ -48,11 +91,15 @@ hipError_t launch_libsvm(const LibsvmArgs &a, uint64_t *res, int phase, hipStrea
     if (phase != kPhaseFill) {
       libsvm_tile<1><<<a.ntiles, kThreads, 0, s>>>(a);
       tile_scan_kernel<<<1, kThreads, 0, s>>>(a.tile_cnt, const_cast<uint64_t *>(a.tile_base), a.ntiles,
-                                              res, a.offset, a.cap[C_ROWS]);
+                                              res, a.offset, a.cap[C_ROWS], gate);
     }
-    if (phase != kPhaseCount) libsvm_tile<2><<<a.ntiles, kThreads, 0, s>>>(a);
+    if (phase != kPhaseCount) {
+      if (!use_fast) prof_mark(0, s, "libsvm_tile<2>");
+      libsvm_tile<2><<<a.ntiles, kThreads, 0, s>>>(a);
+      if (!use_fast) prof_mark(1, s, "libsvm_tile<2>");
+    }
   }
-  finalize_kernel<<<1, 1, 0, s>>>(res);
+  select_kernel<<<1, 1, 0, s>>>(res, gate, f.err);
   return hipGetLastError();
 }
 

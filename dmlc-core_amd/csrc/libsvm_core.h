@@ -292,6 +292,7 @@ DA_HDF uint64_t first_line_start(const LibsvmArgs &a, BK &bk, uint64_t from, uin
 // The tile body.  MODE 1 = count pass, MODE 2 = write pass.
 template <int MODE, class BK>
 DA_HDF void tile(const LibsvmArgs &a, Shared &sh, BK &bk, uint64_t k) {
+  if (a.gate && *a.gate == 0) return;  // the uniform-grammar kernel handled this input
   const uint64_t tlo = k * a.tile_bytes;
   if (tlo >= a.n) return;
   const uint64_t thi = mn(tlo + a.tile_bytes, a.n);

@@ -22,7 +22,8 @@ struct Cnt64Add {
 // offset[total_rows] = total index count (the reference's final offset push).
 __global__ void __launch_bounds__(kThreads)
 tile_scan_kernel(const uint64_t *tile_cnt, uint64_t *tile_base, uint32_t ntiles, uint64_t *res,
-                 uint64_t *offset, uint64_t cap_rows) {
+                 uint64_t *offset, uint64_t cap_rows, const uint32_t *gate) {
+  if (gate && *gate == 0) return;
   __shared__ uint64_t scratch[kBlockScratchU64];
   DevBlock bk{scratch};
   const uint32_t per = (ntiles + kThreads - 1) / kThreads;

@@ -18,6 +18,7 @@ F32, I32, I64 = 0, 1, 2
 ROWS, INDEX, VALUE, WEIGHT, QID, LABEL, FIELD = range(7)
 FLAG_COUNT_ONLY = 1
 FLAG_FILL_ONLY = 2
+FLAG_EXACT = 4
 ERR_CAPACITY = 16
 _FMT = {"libsvm": LIBSVM, "csv": CSV, "libfm": LIBFM}
 _VT = {"f32": F32, "float32": F32, "i32": I32, "int32": I32, "i64": I64, "int64": I64}
@@ -62,12 +63,29 @@ def lib():
         L.dmlc_amd_strtof_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                             ctypes.c_void_p]
+        L.dmlc_amd_profile_begin.restype = ctypes.c_int
+        L.dmlc_amd_profile_end.restype = ctypes.c_int
+        L.dmlc_amd_profile_end.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int),
+                                           ctypes.POINTER(ctypes.c_char_p)]
         _LIB = L
     return _LIB
 
 
+def profile_begin():
+    lib().dmlc_amd_profile_begin()
+
+
+def profile_end():
+    """-> (summed kernel ms, launches, kernel name) since profile_begin()."""
+    t, n, k = ctypes.c_double(0), ctypes.c_int(0), ctypes.c_char_p()
+    if lib().dmlc_amd_profile_end(ctypes.byref(t), ctypes.byref(n), ctypes.byref(k)) != 0:
+        raise RuntimeError("dmlc_amd_profile_end failed")
+    return t.value, n.value, (k.value or b"").decode()
+
+
 EXPORTED_SYMBOLS = ("dmlc_amd_parse", "dmlc_amd_workspace_bytes", "dmlc_amd_error_string",
-                    "dmlc_amd_device_count", "dmlc_amd_abi_version", "dmlc_amd_strtof_batch")
+                    "dmlc_amd_device_count", "dmlc_amd_abi_version", "dmlc_amd_strtof_batch",
+                    "dmlc_amd_profile_begin", "dmlc_amd_profile_end")
 
 
 def make_params(fmt="libsvm", index_bits=32, value_type="f32", indexing_mode=0, label_column=-1,
@@ -197,6 +215,7 @@ class DeviceParser:
                         chunk_table=out["chunk_table"] if nchunks > 0 else None, stream=stream)
         r = res.cpu().numpy().view(np.uint64)
         out["error"] = int(r[8])
+        out["path"] = int(r[9])
         out["result_counts"] = [int(x) for x in r[:8]]
         return out
 
@@ -228,7 +247,7 @@ def to_host(out, index_bits=32, value_type=F32):
     return h
 
 
-def parse_bytes(data, chunk_offsets=None, fmt="libsvm", **kw):
+def parse_bytes(data, chunk_offsets=None, fmt="libsvm", exact=False, **kw):
     """Convenience: host bytes -> device -> parse -> host numpy dict."""
     torch = _torch()
     raw = data.encode("latin-1") if isinstance(data, str) else bytes(data)
@@ -237,11 +256,14 @@ def parse_bytes(data, chunk_offsets=None, fmt="libsvm", **kw):
     text = torch.frombuffer(bytearray(raw), dtype=torch.uint8).cuda() if raw else \
         torch.empty(0, dtype=torch.uint8, device="cuda")
     cs = torch.tensor(np.asarray(chunk_offsets, dtype=np.int64), device="cuda")
+    if exact:
+        kw["flags"] = kw.get("flags", 0) | FLAG_EXACT
     p = DeviceParser(fmt, **kw)
     out = p.parse(text, cs)
     h = to_host(out, p.params.index_bits,
                 p.params.value_type if p.params.format == CSV else F32)
     h["error"] = out["error"]
+    h["path"] = "exact" if out["path"] else "fast"
     h["counts"] = out["counts"]
     return h
 

@@ -83,6 +83,9 @@ typedef struct dmlc_amd_params {
  * the same stream).  COUNT_ONLY then FILL_ONLY does exactly the work of one
  * full call, with a host-side allocation in between. */
 #define DMLC_AMD_FLAG_FILL_ONLY 2u
+/* Skip the single-pass uniform-grammar kernel and run the exact tile kernels
+ * only (results are identical either way; this exists for testing/profiling). */
+#define DMLC_AMD_FLAG_EXACT 4u
 
 typedef struct dmlc_amd_csr {
   uint64_t *offset; /* rows + 1 (global, rebased across chunks) */
@@ -98,7 +101,8 @@ typedef struct dmlc_amd_csr {
 typedef struct dmlc_amd_result {
   uint64_t count[8]; /* exact totals per slot, even when a capacity was exceeded */
   uint64_t error;    /* 0, or (byte position << 16) | error code of the first error */
-  uint64_t reserved[7];
+  uint64_t path;     /* libsvm: 0 = single-pass uniform-grammar kernel, else exact tile kernels */
+  uint64_t reserved[6];
 } dmlc_amd_result;
 
 /* Bytes of device workspace dmlc_amd_parse needs for this input. */
@@ -119,6 +123,14 @@ int dmlc_amd_parse(const void *d_text, uint64_t nbytes, const uint64_t *d_chunk_
  * literal" flag (strtonum.h:163); d_consumed / d_nan_error may be NULL. */
 int dmlc_amd_strtof_batch(const void *d_text, const uint64_t *d_offsets, uint64_t n, float *d_out,
                           uint32_t *d_consumed, uint32_t *d_nan_error, void *stream);
+
+/* Kernel timing for benchmarks: between profile_begin and profile_end, every
+ * dmlc_amd_parse on this thread brackets its dominant kernel (the single-pass
+ * kernel, or the exact write kernel) with HIP events on its stream.
+ * profile_end synchronises, returns the summed kernel time, the number of
+ * bracketed launches and the kernel's name. */
+int dmlc_amd_profile_begin(void);
+int dmlc_amd_profile_end(double *total_ms, int *launches, const char **kernel);
 
 /* Human-readable message for an error code (matches the reference's CHECK text). */
 const char *dmlc_amd_error_string(int code);

@@ -15,6 +15,7 @@
 #include "csv_core.h"
 #include "dmlc_amd.h"
 #include "libsvm_core.h"
+#include "svm_fast.h"
 
 using namespace dmlc_amd;
 
@@ -112,6 +113,13 @@ extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *c
   unsigned long long *err = reinterpret_cast<unsigned long long *>(res + 8);
   if (!ntiles && !count_only && out->offset) out->offset[0] = 0;
   if (prm->format == DMLC_AMD_LIBSVM) {
+    // mirrors launch_libsvm (libsvm.hip): uniform-grammar kernel first, exact
+    // tile kernels when it sets the gate (or indexing_mode < 0 / FLAG_EXACT)
+    const bool use_fast = nbytes > 0 && prm->indexing_mode >= 0 && !(prm->flags & DMLC_AMD_FLAG_EXACT);
+    const uint64_t nft = (nbytes + fsvm::kTile - 1) / fsvm::kTile;
+    uint32_t gate = use_fast ? 0u : 1u, ticket = 0;
+    unsigned long long ferr = ~0ull;
+    std::vector<uint64_t> lb(nft * 4 + 1, 0);
     LibsvmArgs a;
     std::memset(&a, 0, sizeof(a));
     a.text = text;
@@ -134,21 +142,57 @@ extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *c
     a.chunk_tab = chunk_table ? chunk_table : sink.data();
     a.chunk_min = chunk_min.data();
     a.err = err;
-    for (uint64_t k = 0; k < ntiles; ++k) {
-      svm::Shared *sh = new svm::Shared;
-      std::memset(sh, 0xCD, sizeof(*sh));  // LDS is uninitialised on the GPU
-      run_block([&](HostBlock &bk) { svm::tile<1>(a, *sh, bk, k); });
-      delete sh;
-    }
-    tile_scan(tile_cnt, tile_base, ntiles, res);
-    if (!count_only && out->offset && res[C_ROWS] < out->cap[C_ROWS] + 1) out->offset[res[C_ROWS]] = res[C_INDEX];
-    if (!count_only)
-      for (uint64_t k = 0; k < ntiles; ++k) {
-        svm::Shared *sh = new svm::Shared;
+    a.gate = &gate;
+    if (use_fast) {
+      FastSvmArgs f;
+      std::memset(&f, 0, sizeof(f));
+      f.text = text;
+      f.n = nbytes;
+      f.cs = cs;
+      f.nchunk = nchunks;
+      f.ntiles = (uint32_t)nft;
+      f.wide = a.wide;
+      f.indexing_mode = prm->indexing_mode;
+      f.offset = a.offset;
+      f.label = a.label;
+      f.weight = a.weight;
+      f.index = a.index;
+      f.value = a.value;
+      for (int i = 0; i < 8; ++i) f.cap[i] = out->cap[i];
+      f.chunk_tab = chunk_table;
+      f.lb = lb.data();
+      f.ticket = &ticket;
+      f.gate = &gate;
+      f.err = &ferr;
+      f.res = res;
+      for (uint64_t k = 0; k < nft; ++k) {
+        fsvm::Shared *sh = new fsvm::Shared;
         std::memset(sh, 0xCD, sizeof(*sh));
-        run_block([&](HostBlock &bk) { svm::tile<2>(a, *sh, bk, k); });
+        if (count_only) run_block([&](HostBlock &bk) { fsvm::tile<1>(f, *sh, bk); });
+        else run_block([&](HostBlock &bk) { fsvm::tile<2>(f, *sh, bk); });
         delete sh;
       }
+    }
+    if (gate) {
+      for (uint64_t k = 0; k < ntiles; ++k) {
+        svm::Shared *sh = new svm::Shared;
+        std::memset(sh, 0xCD, sizeof(*sh));  // LDS is uninitialised on the GPU
+        run_block([&](HostBlock &bk) { svm::tile<1>(a, *sh, bk, k); });
+        delete sh;
+      }
+      tile_scan(tile_cnt, tile_base, ntiles, res);
+      if (!count_only && out->offset && res[C_ROWS] < out->cap[C_ROWS] + 1) out->offset[res[C_ROWS]] = res[C_INDEX];
+      if (!count_only)
+        for (uint64_t k = 0; k < ntiles; ++k) {
+          svm::Shared *sh = new svm::Shared;
+          std::memset(sh, 0xCD, sizeof(*sh));
+          run_block([&](HostBlock &bk) { svm::tile<2>(a, *sh, bk, k); });
+          delete sh;
+        }
+    } else {
+      res[8] = ferr;
+    }
+    std::fprintf(stderr, "emu: libsvm path=%s\n", gate ? "exact" : "fast");
   } else if (prm->format == DMLC_AMD_CSV) {
     CsvArgs a;
     std::memset(&a, 0, sizeof(a));
@@ -247,9 +291,10 @@ int main(int argc, char **argv) {
   uint64_t res[16];
   dmlc_amd_csr csr;
   std::memset(&csr, 0, sizeof(csr));
-  prm.flags = DMLC_AMD_FLAG_COUNT_ONLY;
+  const uint32_t xf = std::getenv("EMU_EXACT") ? DMLC_AMD_FLAG_EXACT : 0u;
+  prm.flags = DMLC_AMD_FLAG_COUNT_ONLY | xf;
   emu_parse(t, text.size(), cs.data(), nch, &prm, &csr, nullptr, res);
-  prm.flags = 0;
+  prm.flags = xf;
   const size_t vsz = prm.value_type == DMLC_AMD_I64 ? 8 : 4, isz = prm.index_bits == 64 ? 8 : 4;
   std::vector<uint64_t> offset(res[0] + 1);
   void *label = std::malloc(res[5] * vsz + 1), *value = std::malloc(res[2] * vsz + 1),

@@ -23,7 +23,7 @@ def build():
 
 
 def parse(data, chunk_offsets=None, fmt="libsvm", index_bits=32, value_type=0, indexing_mode=0,
-          label_column=-1, weight_column=-1, delimiter=",", tile_bytes=0):
+          label_column=-1, weight_column=-1, delimiter=",", tile_bytes=0, exact=False):
     if not _BUILT:
         build()
     raw = data.encode("latin-1") if isinstance(data, str) else bytes(data)
@@ -36,6 +36,9 @@ def parse(data, chunk_offsets=None, fmt="libsvm", index_bits=32, value_type=0, i
         np.asarray(chunk_offsets, dtype=np.uint64).tofile(cp)
         d = ord(delimiter) if isinstance(delimiter, str) else int(delimiter)
         env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=0:exitcode=77")
+        env.pop("EMU_EXACT", None)
+        if exact:
+            env["EMU_EXACT"] = "1"
         r = subprocess.run([EXE, str(f), str(index_bits), str(int(value_type)), str(indexing_mode),
                             str(label_column), str(weight_column), str(d), str(tile_bytes), tp, cp, op],
                            capture_output=True, env=env)
@@ -55,5 +58,6 @@ def parse(data, chunk_offsets=None, fmt="libsvm", index_bits=32, value_type=0, i
             "chunk_table": np.fromfile(op + ".chunks", dtype=np.uint64).reshape(-1, 8),
             "error": int(res[8]),
             "counts": [int(x) for x in res[:8]],
+            "path": "fast" if b"path=fast" in r.stderr else "exact",
         }
         return h

@@ -1,0 +1,90 @@
+"""Random libsvm text generators for parity tests (emulator and GPU).
+
+uniform_libsvm() draws from the grammar the single-pass kernel handles
+(svm_fast.h: digitchar runs, blanks, ':' and newlines, including the odd
+corners of ParsePair -- runs of signs/dots/exponents, stray colons after a
+newline, CR/LF mixes, tabs, label:weight, missing values, very long runs and
+gaps).  With violate=True it also injects the constructs that must send the
+input to the exact kernels ('#', "qid:", letters, dangling "x:", "a:b:c").
+"""
+import numpy as np
+
+_NUM = ["0", "1", "7", "42", "007", "+3", "-0", "0.5", ".5", "5.", "1e-3", "-2.5E+7", "3.4028235e38",
+        "1e39", "1e-45", "123456789012345678901234", "0.123456789012345678901234", "+", "-", ".",
+        "e", "E5", "1e", "1.5e-", "--1", "+-2", "9" * 30]
+
+
+def _num(rng):
+    if rng.random() < 0.6:
+        return "%.9g" % rng.random() if rng.random() < 0.7 else str(int(rng.integers(0, 10 ** 6)))
+    return _NUM[int(rng.integers(0, len(_NUM)))]
+
+
+def _idx(rng):
+    if rng.random() < 0.85:
+        return str(int(rng.integers(0, 5000)))
+    return ["0", "4294967297", "+12", "3.7", "1e3", "00", "18446744073709551617"][int(rng.integers(0, 7))]
+
+
+def _blank(rng):
+    r = rng.random()
+    if r < 0.8:
+        return " "
+    if r < 0.9:
+        return "\t"
+    return " " * int(rng.integers(2, 90))
+
+
+def _line(rng, maxfeat, violate):
+    parts = []
+    if rng.random() < 0.1:
+        parts.append(_blank(rng))
+    if rng.random() < 0.05:
+        parts.append(":")  # colon before the label: skipped by ParsePair
+    parts.append(_num(rng))
+    if rng.random() < 0.15:
+        parts.append(rng.choice([":", " :", ": ", " : "]) + _num(rng))
+    for _ in range(int(rng.integers(0, maxfeat + 1))):
+        parts.append(_blank(rng))
+        parts.append(_idx(rng))
+        if rng.random() < 0.93:
+            parts.append(rng.choice([":", ":", ":", " :", ": ", ":\t"]) + _num(rng))
+    if violate and rng.random() < 0.2:
+        parts.append(rng.choice([" # c", " qid:3", " 3:", " 1:2:3", "x", " 2:nan", " 5:inf", ":"]))
+    if rng.random() < 0.1:
+        parts.append(_blank(rng))
+    return "".join(parts)
+
+
+def uniform_libsvm(rng, nlines, maxfeat=40, violate=False):
+    out = []
+    for _ in range(nlines):
+        r = rng.random()
+        if r < 0.04:
+            out.append("")  # blank line
+        elif r < 0.06:
+            out.append(_blank(rng))
+        else:
+            out.append(_line(rng, maxfeat, violate))
+    seps = ["\n"] * 12 + ["\r\n", "\r", "\n\n"]
+    text = "".join(line + seps[int(rng.integers(0, len(seps)))] for line in out)
+    if rng.random() < 0.3:
+        text = text.rstrip("\r\n")  # no trailing newline
+    return text.encode("latin-1")
+
+
+def random_cuts(rng, data, nmax=8, anywhere=False):
+    """Chunk offsets: after a newline (as an InputSplit cuts), or, with
+    anywhere=True, at arbitrary bytes (the C-ABI allows any chunking)."""
+    n = len(data)
+    if n == 0:
+        return [0]
+    if anywhere:
+        cand = list(range(1, n))
+    else:
+        a = np.frombuffer(data, dtype=np.uint8)
+        cand = (np.flatnonzero((a == 10) | (a == 13)) + 1).tolist()
+        cand = [c for c in cand if c < n]
+    k = int(rng.integers(0, min(nmax, len(cand)) + 1)) if cand else 0
+    cuts = sorted(set(rng.choice(cand, size=k, replace=False).tolist())) if k else []
+    return [0] + cuts + [n]

@@ -6,9 +6,11 @@ catch logic and memory-safety bugs in the kernel bodies without a GPU."""
 import numpy as np
 import pytest
 
+import fuzz_text
 from golden_util import dec, diff, load_cases
 from oracle import pyoracle as po
 from tests.emu import pyemu
+from tools import synth
 
 FMT = {po.LIBSVM: "libsvm", po.CSV: "csv"}
 
@@ -91,3 +93,57 @@ def test_emu_long_lines_small_tiles():
         o = po.parse_chunks(data, [0, len(data)], fmt=po.LIBSVM)
         h = pyemu.parse(data, [0, len(data)], "libsvm", tile_bytes=tile)
         assert h["error"] == 0 and diff(h, o) == []
+
+
+# ---------------------------------------------------------------- fast path --
+
+
+def _emu_vs_oracle(data, offs, exact=False, **kw):
+    o = po.parse_chunks(data, offs, fmt=po.LIBSVM, **kw)
+    h = pyemu.parse(data, offs, "libsvm", exact=exact, **kw)
+    failed = check_fail(h, "libsvm", offs)
+    assert (o["status"] != 0) == failed, (data[:200], offs, kw, o["msg"], h["error"])
+    if not failed:
+        assert diff(h, o) == [], (diff(h, o), offs, kw)
+    return h
+
+
+def test_emu_fast_fuzz_vs_oracle():
+    """Uniform-grammar inputs (single tile) with violations and odd chunkings:
+    whichever path runs, the result is the reference's."""
+    rng = np.random.default_rng(2024)
+    paths = {"fast": 0, "exact": 0}
+    for it in range(50):
+        data = fuzz_text.uniform_libsvm(rng, int(rng.integers(1, 30)), int(rng.integers(0, 30)),
+                                        violate=rng.random() < 0.3)
+        offs = fuzz_text.random_cuts(rng, data, 5, anywhere=rng.random() < 0.3)
+        kw = {}
+        if rng.random() < 0.2:
+            kw["index_bits"] = 64
+        if rng.random() < 0.2:
+            kw["indexing_mode"] = 1
+        paths[_emu_vs_oracle(data, offs, **kw)["path"]] += 1
+    assert paths["fast"] > 20 and paths["exact"] > 5, paths
+
+
+def test_emu_fast_multi_tile():
+    """Inputs spanning several 16 KiB tiles: look-back across tiles, runs and
+    lines crossing tile ends, long gaps, chunk starts at arbitrary bytes."""
+    rng = np.random.default_rng(77)
+    for it in range(4):
+        data = fuzz_text.uniform_libsvm(rng, 300, 60)
+        offs = fuzz_text.random_cuts(rng, data, 8, anywhere=it % 2 == 1)
+        h = _emu_vs_oracle(data, offs)
+        assert len(data) > 3 * 16384
+        if it % 2 == 0:
+            assert h["path"] == "fast"
+
+
+def test_emu_fast_equals_exact_synthetic():
+    text, _ = synth.rows(synth.LIBSVM, 800, 40, seed=5)
+    data = text.tobytes()
+    offs = [0, len(data) // 2 + data[len(data) // 2:].index(b"\n") + 1, len(data)]
+    hf = _emu_vs_oracle(data, offs)
+    he = _emu_vs_oracle(data, offs, exact=True)
+    assert hf["path"] == "fast" and he["path"] == "exact"
+    assert hf["chunk_table"].tolist() == he["chunk_table"].tolist()

@@ -195,3 +195,95 @@ def test_gpu_empty_and_tiny(dm):
         for d in (b"", b"\n", b"\r\n\r\n", b"1", b"1\n", b"   \n"):
             offs = [0, len(d)] if d else [0]
             _oracle_vs_gpu(dm, d, offs, fmt)
+
+
+# ------------------------------------------------- single-pass fast path --
+import fuzz_text  # noqa: E402
+
+
+def _gpu_vs_oracle_paths(dm, data, offs, **kw):
+    """Default path and forced exact path both equal the oracle."""
+    o = po.parse_chunks(data, offs, fmt=po.LIBSVM, **kw)
+    res = {}
+    for exact in (False, True):
+        h = dm.parse_bytes(data, offs, fmt="libsvm", exact=exact, **kw)
+        nch = len(offs) - 1
+        failed = bool(h["error"]) or (nch > 0 and dm.chunk_check(h, "libsvm", nch, h["counts"]) >= 0)
+        assert (o["status"] != 0) == failed, (exact, o["msg"], h["error"], data[:200], offs, kw)
+        if not failed:
+            bad = diff(h, o)
+            assert bad == [], (exact, bad, offs, kw)
+        res[exact] = h
+    if o["status"] == 0:
+        assert res[False]["chunk_table"].tolist() == res[True]["chunk_table"].tolist()
+    return res[False]
+
+
+def test_gpu_fast_fuzz_vs_oracle(dm):
+    rng = np.random.default_rng(31337)
+    paths = {"fast": 0, "exact": 0}
+    for it in range(400):
+        data = fuzz_text.uniform_libsvm(rng, int(rng.integers(1, 40)), int(rng.integers(0, 40)),
+                                        violate=rng.random() < 0.25)
+        offs = fuzz_text.random_cuts(rng, data, 6, anywhere=rng.random() < 0.3)
+        kw = {}
+        if rng.random() < 0.2:
+            kw["index_bits"] = 64
+        if rng.random() < 0.2:
+            kw["indexing_mode"] = int(rng.integers(0, 2))
+        try:
+            paths[_gpu_vs_oracle_paths(dm, data, offs, **kw)["path"]] += 1
+        except AssertionError as e:
+            raise AssertionError("case %d: %s" % (it, e))
+    assert paths["fast"] > 200, paths
+
+
+def test_gpu_fast_multi_tile_vs_oracle(dm):
+    rng = np.random.default_rng(4711)
+    for it in range(24):
+        data = fuzz_text.uniform_libsvm(rng, int(rng.integers(200, 3000)), int(rng.integers(1, 120)),
+                                        violate=it % 6 == 5)
+        offs = fuzz_text.random_cuts(rng, data, int(rng.integers(0, 40)), anywhere=it % 3 == 1)
+        h = _gpu_vs_oracle_paths(dm, data, offs)
+        if it % 6 != 5 and it % 3 != 1:
+            assert h["path"] == "fast", it
+
+
+def test_gpu_fast_synthetic_vs_oracle(dm):
+    """~100 MB of canonical synthetic text (many tiles, 8 MiB InputSplit chunks)."""
+    text, _ = synth.rows(synth.LIBSVM, 50000, 128, seed=21)
+    offs = dm.text_chunk_starts(text, 8 << 20).tolist()
+    o = po.parse_chunks(text.tobytes(), offs, fmt=po.LIBSVM)
+    h = dm.parse_bytes(text.tobytes(), offs, fmt="libsvm")
+    assert h["path"] == "fast" and h["error"] == 0
+    assert diff(h, o) == []
+
+
+def test_gpu_fast_equals_exact_bench_size(dm):
+    """Bench-size input (BASELINE config 2, 1M rows x 128 nnz): the single-pass
+    kernel and the exact kernels agree bit for bit (the exact kernels are
+    pinned to the oracle above); plus size-independent CSR properties."""
+    import torch
+    text, _ = synth.rows(synth.LIBSVM, 1 << 20, 128, seed=1)
+    starts = dm.text_chunk_starts(text)
+    d_text = torch.from_numpy(text).cuda()
+    d_cs = torch.from_numpy(starts).cuda()
+    outs = {}
+    for exact in (False, True):
+        p = dm.DeviceParser("libsvm", flags=dm.FLAG_EXACT if exact else 0)
+        out = p.parse(d_text, d_cs)
+        assert out["error"] == 0 and out["path"] == (1 if exact else 0)
+        outs[exact] = out
+    c = outs[False]["counts"]
+    assert c == outs[True]["counts"]
+    assert c[dm.ROWS] == 1 << 20 and c[dm.INDEX] == 128 << 20 and c[dm.VALUE] == 128 << 20
+    for k in ("offset", "label", "index", "value"):
+        a, b = outs[False][k], outs[True][k]
+        assert torch.equal(a.view(torch.int32) if a.dtype == torch.float32 else a,
+                           b.view(torch.int32) if b.dtype == torch.float32 else b), k
+    off = outs[False]["offset"]
+    assert bool((off[1:] - off[:-1] == 128).all())
+    idx = outs[False]["index"].view(-1, 128).to(torch.int64)
+    assert bool((idx[:, 1:] > idx[:, :-1]).all())  # generator: strictly increasing ids
+    v = outs[False]["value"]
+    assert bool(((v >= 0) & (v < 1)).all())
