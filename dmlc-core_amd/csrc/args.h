@@ -46,7 +46,7 @@ struct FastSvmArgs {
   float *value;
   uint64_t cap[8];
   uint64_t *chunk_tab;  // may be null
-  uint64_t *lb;         // [ntiles][4] look-back words, zeroed per launch
+  uint64_t *lb;         // [ntiles][8] look-back records, zeroed per launch
   uint32_t *ticket;     // tile ticket counter, zeroed per launch
   uint32_t *gate;       // != 0: input left the grammar -> exact path
   unsigned long long *err;  // first error of this path

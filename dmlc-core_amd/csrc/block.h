@@ -11,6 +11,14 @@ struct DevBlock {
 
   __device__ __forceinline__ int tid() const { return threadIdx.x; }
   __device__ __forceinline__ void sync() const { __syncthreads(); }
+  // wave-level: ballot over the 64 lanes, and an LDS-ordering point for a
+  // protocol run by one wave (LDS ops of a wave complete in order; the fence
+  // stops the compiler from moving LDS accesses across it)
+  __device__ __forceinline__ uint64_t ballot(bool p) const { return __ballot(p); }
+  __device__ __forceinline__ void wave_sync() const {
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
 
   template <typename T>
   __device__ __forceinline__ static T shfl_up(T v, int d) {

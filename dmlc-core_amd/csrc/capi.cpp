@@ -52,6 +52,7 @@ struct Profile {
   const char *kernel = "";
 };
 thread_local Profile g_prof;
+thread_local hipError_t g_last_hip = hipSuccess;
 
 }  // namespace
 
@@ -129,7 +130,7 @@ size_t dmlc_amd_workspace_bytes(uint64_t nbytes, int nchunks, const dmlc_amd_par
   const uint64_t ntiles = (nbytes + T - 1) / T;
   const uint64_t nc = nchunks > 0 ? (uint64_t)nchunks : 1;
   const uint64_t nft = (nbytes + kFastTile - 1) / kFastTile;
-  return (size_t)((2 * ntiles * kSlots + nc + nc * 8 + nft * 4) * sizeof(uint64_t) + 11 * 256);
+  return (size_t)((2 * ntiles * kSlots + nc + nc * 8 + nft * 8) * sizeof(uint64_t) + 11 * 256);
 }
 
 int dmlc_amd_parse(const void *d_text, uint64_t nbytes, const uint64_t *d_chunk_starts, int nchunks,
@@ -159,7 +160,7 @@ int dmlc_amd_parse(const void *d_text, uint64_t nbytes, const uint64_t *d_chunk_
   const uint64_t nft = (nbytes + kFastTile - 1) / kFastTile;
   uint32_t *ctl = cv.take<uint32_t>(4);               // gate, ticket
   unsigned long long *ferr = cv.take<unsigned long long>(1);
-  uint64_t *lb = cv.take<uint64_t>(nft * 4 + 1);
+  uint64_t *lb = cv.take<uint64_t>(nft * 8 + 1);
   if (!tile_cnt || !tile_base || !chunk_min || !chunk_sink || !ctl || !ferr || !lb) return DMLC_AMD_ERR_ARG;
   uint64_t *res = reinterpret_cast<uint64_t *>(d_result);
   const bool count_only = (prm->flags & DMLC_AMD_FLAG_COUNT_ONLY) != 0;
@@ -245,7 +246,10 @@ int dmlc_amd_parse(const void *d_text, uint64_t nbytes, const uint64_t *d_chunk_
   } else {
     return DMLC_AMD_ERR_ARG;  // libfm: not built yet
   }
+  g_last_hip = e;
   return e == hipSuccess ? DMLC_AMD_OK : DMLC_AMD_ERR_HIP;
 }
+
+const char *dmlc_amd_last_hip_error(void) { return hipGetErrorString(g_last_hip); }
 
 }  // extern "C"

@@ -33,6 +33,14 @@ DA_HD void atomic_or_u32(uint32_t *p, uint32_t v) {
 #endif
 }
 
+DA_HD void atomic_or_u64(uint64_t *p, uint64_t v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  atomicOr((unsigned long long *)p, (unsigned long long)v);
+#else
+  __atomic_fetch_or(p, v, __ATOMIC_RELAXED);
+#endif
+}
+
 DA_HD void atomic_min_u64(unsigned long long *p, unsigned long long v) {
 #if defined(__HIP_DEVICE_COMPILE__)
   atomicMin(p, v);

@@ -64,7 +64,7 @@ hipError_t launch_libsvm(const LibsvmArgs &a, const FastSvmArgs &f, bool use_fas
   if (use_fast) {
     if ((e = hipMemsetAsync(f.ticket, 0, sizeof(uint32_t), s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(f.err, 0xFF, sizeof(uint64_t), s)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(f.lb, 0, (size_t)f.ntiles * 4 * sizeof(uint64_t), s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(f.lb, 0, (size_t)f.ntiles * 8 * sizeof(uint64_t), s)) != hipSuccess) return e;
     if (phase == kPhaseCount) {
       prof_mark(0, s, "svm_fast_tile<1>");
       svm_fast_tile<1><<<f.ntiles, kThreads, 0, s>>>(f);
@@ -104,3 +104,11 @@ hipError_t launch_libsvm(const LibsvmArgs &a, const FastSvmArgs &f, bool use_fas
 }
 
 }  // namespace dmlc_amd
+
+#if defined(DMLC_AMD_STAMPS)
+// diagnostic build: copy the phase stamps of the last launch to the host
+extern "C" int dmlc_amd_debug_stamps(void *dst, size_t bytes) {
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(dmlc_amd::fsvm::g_stamps), bytes, 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? 0 : 33;
+}
+#endif

@@ -15,8 +15,8 @@
 // thread) plus a short look-back to the previous run.  The kernel is single
 // pass: a tile (16 KiB, 256 threads) classifies its bytes, publishes its
 // counts, finds its output base by decoupled look-back over earlier tiles,
-// then decodes its runs token-parallel (one run per thread per step), writing
-// index / value / label coalesced.  Any byte or structure outside the grammar
+// then each thread decodes its own segment's runs role by role (SWAR digit
+// conversion from LDS) and stores them.  Any byte or structure outside the grammar
 // sets the gate word; the launcher then runs the exact tile kernels
 // (libsvm_core.h) instead, so results are always the reference's.
 //
@@ -35,12 +35,34 @@ constexpr int kPre = 64;                 // staged bytes before the tile (look-b
 constexpr int kPost = 128;               // staged bytes after it (runs crossing the end)
 constexpr int kStage = kPre + kTile + kPost;
 constexpr int kMaxCs = 32;               // chunk starts per tile the fast path accepts
-constexpr int kMaxRuns = kTile / 2 + kMaxCs + 2;
 constexpr uint64_t kAgg = 1ull << 62, kIncl = 2ull << 62, kValMask = (1ull << 62) - 1;
 constexpr uint32_t kSpinLimit = 1u << 26;
 
 enum : uint32_t { R_NONE = 0, R_L = 1, R_K = 2, R_I = 3 };
-// look-back counter slots
+
+// Diagnostic build only (-DDMLC_AMD_STAMPS, libdmlc_amd_stamps.so): thread 0
+// of each tile records s_memtime at phase boundaries into g_stamps; the
+// product build executes no stamp.
+constexpr uint32_t kStampTiles = 1u << 17;
+#if defined(DMLC_AMD_STAMPS) && defined(__HIPCC__)
+__device__ uint64_t g_stamps[kStampTiles * 8];
+#endif
+#if defined(DMLC_AMD_STAMPS) && defined(__HIP_DEVICE_COMPILE__)
+#define FSVM_STAMP(k, i)                                                         \
+  do {                                                                           \
+    if (tid == 0 && (k) < kStampTiles) {                                         \
+      __builtin_amdgcn_sched_barrier(0);                                         \
+      g_stamps[(uint64_t)(k) * 8 + (i)] =                                        \
+          (i) == 0 ? __builtin_amdgcn_s_memrealtime() : __builtin_amdgcn_s_memtime(); \
+      __builtin_amdgcn_sched_barrier(0);                                         \
+    }                                                                            \
+  } while (0)
+#else
+#define FSVM_STAMP(k, i) \
+  do {                   \
+  } while (0)
+#endif
+// look-back counter slots (record words 0-3: aggregate, 4-7: inclusive prefix)
 enum { Q_ROWS = 0, Q_INDEX = 1, Q_VALUE = 2, Q_WEIGHT = 3 };
 
 // Byte classes by two 16-entry nibble tables (v_perm_b32 lookups): cls =
@@ -83,9 +105,22 @@ DA_HD void load16(const uint8_t *p, uint32_t w[4]) {
 #endif
 }
 
-// Masks of the 64 bytes at p (16-byte aligned); bytes >= nvalid are outside
-// the text and classify as blanks.
-DA_HD Masks classify64(const uint8_t *p, int nvalid) {
+struct Nib {
+  uint32_t d, n, c, bad;
+};
+DA_HD Nib classify_dword(uint32_t x) {  // 4-bit masks of 4 bytes; bad: a byte outside the grammar
+  const uint32_t cls = classify4(x);
+  Nib r;
+  r.d = nib_d(cls);
+  r.n = nib_n(cls);
+  r.c = nib_c(cls);
+  r.bad = ((cls + 0x7F7F7F7Fu) & 0x80808080u) != 0x80808080u || (x & 0x80808080u);
+  return r;
+}
+
+// Masks of the 64 bytes at p (16-byte aligned).  Bytes past the end of the
+// text are staged as blanks, so they are neutral here.
+DA_HD Masks classify64(const uint8_t *p) {
   uint32_t dl = 0, dh = 0, nl = 0, nh = 0, cl = 0, ch = 0;
   uint32_t all = 0x80808080u, orv = 0;
 #pragma unroll
@@ -95,14 +130,8 @@ DA_HD Masks classify64(const uint8_t *p, int nvalid) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int i = 4 * q + j;
-      uint32_t x = w[j];
-      uint32_t cls = classify4(x);
-      const int nb = nvalid - 4 * i;
-      if (nb < 4) {
-        const uint32_t vm = nb <= 0 ? 0u : ((1u << (8 * nb)) - 1u);
-        cls = (cls & vm) | (0x20202020u & ~vm);
-        x &= vm;
-      }
+      const uint32_t x = w[j];
+      const uint32_t cls = classify4(x);
       all &= cls + 0x7F7F7F7Fu;
       orv |= x;
       const int sh = 4 * (i & 7);
@@ -130,22 +159,164 @@ struct Shared {  // LDS of one workgroup
   uint64_t md[kThreads + 1];          // slot 0: the segment before the tile; slot t+1: segment t
   uint64_t mn[kThreads + 1];
   uint64_t mc[kThreads + 1];
-  uint16_t runs[kMaxRuns];            // run starts (tile-relative), grouped L | W | I | V
   uint64_t csl[kMaxCs + 1];           // chunk starts in [tlo, thi]
   uint64_t cfloor, cnext, base[4];
-  uint32_t ncs, c_first, tile, tot[5];
+  uint64_t lbw[4 * kWave];            // look-back round: values per lane and counter
+  uint32_t ncs, c_first, tile, toomany, bad;
 };
 
-struct Cnt5 {
-  uint32_t c[5];  // L, W, I, V, bad
+struct AddU64 {
+  DA_HD uint64_t operator()(uint64_t a, uint64_t b) const { return a + b; }
 };
-struct Cnt5Add {
-  DA_HD Cnt5 operator()(const Cnt5 &a, const Cnt5 &b) const {
-    Cnt5 r;
-    for (int i = 0; i < 5; ++i) r.c[i] = a.c[i] + b.c[i];
-    return r;
+
+// ---- SWAR decoders on the first 16 bytes of a run (read from the staged LDS
+// text with five aligned words).  Digits are located with byte-parallel masks
+// and converted eight at a time (multiply-shift 8-digit conversion), then
+// combined with exactly the reference's arithmetic.
+
+DA_HD uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t sft) {  // ((hi:lo) >> sft), sft < 32
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_alignbit(hi, lo, sft);
+#else
+  return (uint32_t)((((uint64_t)hi << 32) | lo) >> sft);
+#endif
+}
+
+DA_HD uint32_t nondigit8(uint64_t x) {  // bit i: byte i is not '0'..'9' (grammar bytes < 0x80)
+  const uint64_t t = x ^ 0x3030303030303030ull;
+  const uint64_t h = ((t + 0x7676767676767676ull) & 0x8080808080808080ull) >> 7;
+  return (uint32_t)((h * 0x0102040810204080ull) >> 56);
+}
+
+DA_HD uint64_t parse8(uint64_t w) {  // 8 ASCII digits, first char in the low byte
+  w = ((w & 0x0F0F0F0F0F0F0F0Full) * 2561ull) >> 8;
+  w = ((w & 0x00FF00FF00FF00FFull) * 6553601ull) >> 16;
+  return ((w & 0x0000FFFF0000FFFFull) * 42949672960001ull) >> 32;
+}
+
+struct W16 {
+  uint64_t lo, hi;  // window bytes 0..7, 8..15
+  DA_HD uint32_t byte(uint32_t p) const {
+    return (uint32_t)((p < 8 ? lo >> (8 * p) : hi >> (8 * (p - 8))) & 0xFFu);
   }
+  DA_HD uint64_t at(uint32_t a) const {  // bytes a .. a+7 (zero beyond the window)
+    if (a == 0) return lo;
+    if (a < 8) return (lo >> (8 * a)) | (hi << (64 - 8 * a));
+    return a < 16 ? hi >> (8 * (a - 8)) : 0;
+  }
+  DA_HD uint64_t span8(uint32_t a, uint32_t len) const {  // value of len <= 8 digits at a
+    if (len == 0) return 0;
+    uint64_t w = at(a) << (8 * (8 - len));
+    if (len < 8) w |= 0x3030303030303030ull >> (8 * len);
+    return parse8(w);
+  }
+  DA_HD uint64_t span16(uint32_t a, uint32_t len) const {  // len <= 16
+    return len <= 8 ? span8(a, len) : span8(a, len - 8) * 100000000ull + span8(a + len - 8, 8);
+  }
+  DA_HD uint32_t digits() const { return ~(nondigit8(lo) | (nondigit8(hi) << 8)) & 0xFFFFu; }
 };
+
+DA_HD uint32_t run_len(uint32_t dm, uint32_t a) {  // consecutive digits from byte a
+  return a >= 16 ? 0 : (uint32_t)ctz32(~(dm >> a));
+}
+
+DA_HD double pow10_exact(uint32_t k) {  // 10^k as a double, exact for k <= 22
+  double p = 1.0;
+  if (k & 1u) p *= 10.0;
+  if (k & 2u) p *= 100.0;
+  if (k & 4u) p *= 1e4;
+  if (k & 8u) p *= 1e8;
+  if (k & 16u) p *= 1e16;
+  return p;
+}
+
+// ParseFloat<float> (strtonum.h:95-264) restated for a run of the uniform
+// grammar -- inf / nan / the 'f' suffix need letters outside it -- with the
+// reference's operations: u64 integer part, f32 conversion, one f64 division
+// of the (<= 19-digit) fraction, f32 add, f32 exponent scaling.
+// *ok = false when the number may continue past the window (caller falls back).
+DA_HD float wfloat(const W16 &w, bool *ok) {
+  const uint32_t dm = w.digits();
+  const uint32_t b0 = w.byte(0);
+  const bool sign = b0 != '-';
+  const uint32_t s = (b0 == '-' || b0 == '+') ? 1u : 0u;
+  const uint32_t il = run_len(dm, s);
+  uint32_t p = s + il;
+  *ok = false;
+  if (p >= 16) return 0.f;
+  float value = (float)w.span16(s, il);
+  uint32_t c = w.byte(p);
+  if (c == '.') {
+    const uint32_t fs = p + 1;
+    const uint32_t fl = run_len(dm, fs);
+    p = fs + fl;
+    if (p >= 16) return 0.f;
+    value += (float)((double)w.span16(fs, fl) / pow10_exact(fl));
+    c = w.byte(p);
+  }
+  if (c == 'e' || c == 'E') {
+    bool frac = false;
+    float scale = 1.0f;
+    if (++p >= 16) return 0.f;
+    c = w.byte(p);
+    if (c == '-' || c == '+') {
+      frac = c == '-';
+      if (++p >= 16) return 0.f;
+      c = w.byte(p);
+    }
+    uint32_t expon = 0;
+    for (; is_digit(c); c = w.byte(p)) {
+      expon = expon * 10u + (c - '0');
+      if (++p >= 16) return 0.f;
+    }
+    if (expon > 38u) expon = 38u;
+    const float kMaxSig = (float)3.402823466, kMaxSigNeg = (float)1.175494351;
+    if (expon == 38u && ((!frac && value > kMaxSig) || (frac && value < kMaxSigNeg)))
+      value = frac ? kMaxSigNeg : kMaxSig;
+    while (expon >= 8u) {
+      scale *= 1E8f;
+      expon -= 8u;
+    }
+    while (expon > 0u) {
+      scale *= 10.0f;
+      expon -= 1u;
+    }
+    value = frac ? (value / scale) : (value * scale);
+  }
+  *ok = true;
+  return sign ? value : -value;
+}
+
+// ParseUnsignedInt (strtonum.h:392-428) on a run (no leading blanks there):
+// false on a leading '-' (the reference's fatal CHECK).  Up to 16 digits the
+// exact value truncated to the index width equals the reference's wrapping
+// accumulation.
+DA_HD bool wuint(const W16 &w, bool wide, uint64_t *out, bool *ok) {
+  const uint32_t b0 = w.byte(0);
+  *ok = true;
+  if (b0 == '-') return false;
+  const uint32_t s = b0 == '+' ? 1u : 0u;
+  const uint32_t il = run_len(w.digits(), s);
+  if (s + il >= 16) {
+    *ok = false;
+    return true;
+  }
+  const uint64_t v = w.span16(s, il);
+  *out = wide ? v : (uint64_t)(uint32_t)v;
+  return true;
+}
+
+// the 16 bytes at absolute position q (staged in LDS; q < thi) as a window
+DA_HD W16 win_at(const Shared &sh, uint64_t tlo, uint64_t q) {
+  const uint32_t off = (uint32_t)(q - tlo) + kPre;
+  const uint32_t *w = reinterpret_cast<const uint32_t *>(sh.text + (off & ~3u));
+  const uint32_t sft = (off & 3u) * 8u;
+  const uint32_t x0 = w[0], x1 = w[1], x2 = w[2], x3 = w[3], x4 = w[4];
+  W16 r;
+  r.lo = funnel(x1, x0, sft) | ((uint64_t)funnel(x2, x1, sft) << 32);
+  r.hi = funnel(x3, x2, sft) | ((uint64_t)funnel(x4, x3, sft) << 32);
+  return r;
+}
 
 struct Tile {
   const FastSvmArgs *a;
@@ -162,7 +333,7 @@ struct Tile {
       *c = sh->mc[s];
       return;
     }
-    const Masks m = classify64(a->text + (g << 6), 64);
+    const Masks m = classify64(a->text + (g << 6));
     *d = m.d;
     *n = m.n;
     *c = m.c;
@@ -211,6 +382,41 @@ struct Tile {
   }
 };
 
+// Carry-in at a segment start P from the masks of the 64 bytes before it
+// (bit i <-> P-64+i), when no chunk starts in (P-64, P] and the previous run
+// and its gap lie inside those 64 bytes (the common case).  Returns false
+// when the general look-back (Tile::last_bit) is needed.
+DA_HD bool carry_fast(uint64_t d1, uint64_t n1, uint64_t c1, uint32_t *dc, uint32_t *ginl,
+                      uint32_t *ginc, uint32_t *prole) {
+  *dc = (uint32_t)(d1 >> 63);
+  uint32_t qb;  // first bit of the last run that starts before P
+  if (*dc) {
+    const uint64_t nd = ~d1;
+    if (!nd) return false;
+    qb = 64 - clz64(nd);
+    *ginl = *ginc = 0;
+  } else {
+    if (!d1) return false;
+    const uint32_t pb = 63 - clz64(d1);  // last digitchar, <= 62
+    const uint64_t tg = ~0ull << (pb + 1);
+    const uint64_t tgn = n1 & tg;
+    *ginl = tgn != 0;
+    const uint32_t ln = tgn ? 63 - clz64(tgn) : 0;
+    const uint64_t after = !tgn ? tg : (ln == 63 ? 0ull : ~0ull << (ln + 1));
+    *ginc = (c1 & after) != 0;
+    const uint64_t nd = ~d1 & ((1ull << pb) - 1);
+    if (!nd) return false;
+    qb = 64 - clz64(nd);
+  }
+  // role of the run starting at bit qb (1 <= qb <= 63): its gap is (p2, qb)
+  const uint64_t below = d1 & ((1ull << (qb - 1)) - 1);
+  if (!below) return false;
+  const uint32_t p2 = 63 - clz64(below);
+  const uint64_t gm = ((1ull << qb) - 1) & ~((2ull << p2) - 1);
+  *prole = (n1 & gm) ? R_L : ((c1 & gm) ? R_K : R_I);
+  return true;
+}
+
 // Runs, roles and counts of segment tid (positions P .. P+63).
 struct SegOut {
   uint64_t L, W, I, V;
@@ -235,7 +441,10 @@ DA_HD SegOut segment_roles(const Tile &t, int tid) {
   // ---- carry-in: state just before P
   uint32_t dc = 0, ginl = 0, ginc = 0, prole = R_NONE;
   const uint64_t F = t.floor_of(P);
-  if (P != F) {
+  if (P != F && !(F + 64 <= P &&
+                  carry_fast(t.sh->md[tid], t.sh->mn[tid], t.sh->mc[tid], &dc, &ginl, &ginc, &prole))) {
+    dc = ginl = ginc = 0;
+    prole = R_NONE;
     uint64_t d, n, c;
     t.seg((P - 1) >> 6, &d, &n, &c);
     dc = (uint32_t)(d >> 63) & 1u;
@@ -281,16 +490,6 @@ DA_HD SegOut segment_roles(const Tile &t, int tid) {
   return o;
 }
 
-DA_HD uint32_t lower_count(const uint16_t *r, uint32_t n, uint32_t x) {  // #entries < x (sorted)
-  uint32_t lo = 0, hi = n;
-  while (lo < hi) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (r[mid] < x) lo = mid + 1;
-    else hi = mid;
-  }
-  return lo;
-}
-
 // MODE 1: count only (size query); MODE 2: parse and write.
 template <int MODE, class BK>
 DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk) {
@@ -301,6 +500,8 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk) {
   bk.sync();
   const uint32_t k = sh.tile;
   if (k == ~0u) return;
+  FSVM_STAMP(k, 0);
+  FSVM_STAMP(k, 1);
   Tile t;
   t.a = &a;
   t.sh = &sh;
@@ -322,194 +523,291 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk) {
     }
     sh.ncs = m < kMaxCs ? m : kMaxCs;
     sh.cnext = a.cs[c];  // cs[nchunk] == n
-    sh.tot[4] = m > kMaxCs;
+    sh.toomany = m > kMaxCs;
+    sh.bad = 0;
+    sh.md[0] = sh.mn[0] = sh.mc[0] = 0;
   }
-  // ---- stage [tlo - kPre, thi + kPost) into LDS
+  // ---- stage [tlo - kPre, tlo + kTile + kPost) into LDS; bytes past the end
+  // of the text become blanks (neutral to the classifier; never decoded)
   {
     const uint64_t s0 = t.tlo >= (uint64_t)kPre ? t.tlo - kPre : 0;
-    const uint64_t s1 = mn<uint64_t>(t.thi + kPost, a.n);
+    const uint64_t s1 = t.tlo + kTile + kPost;
     uint8_t *dst = sh.text + (s0 + kPre - t.tlo);
-    const uint64_t nunits = (s1 - s0 + 15) >> 4;
+    const uint64_t nunits = (s1 - s0) >> 4;
     for (uint64_t u = tid; u < nunits; u += kThreads) {
       const uint64_t g = s0 + (u << 4);
+      uint32_t w[4];
       if (g + 16 <= a.n) {
-        uint32_t w[4];
         load16(a.text + g, w);
-        memcpy(dst + (u << 4), w, 16);
       } else {
-        for (int q = 0; q < 16; ++q) dst[(u << 4) + q] = g + q < a.n ? a.text[g + q] : 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          uint32_t x = 0;
+#pragma unroll
+          for (int b = 0; b < 4; ++b) {
+            const uint64_t pos = g + 4 * q + b;
+            x |= (uint32_t)(pos < a.n ? a.text[pos] : (uint8_t)' ') << (8 * b);
+          }
+          w[q] = x;
+        }
       }
+      memcpy(dst + (u << 4), w, 16);
     }
   }
   bk.sync();
-  // ---- classify: segment tid -> slot tid+1; thread 0 also the segment before the tile
+  FSVM_STAMP(k, 2);
+  // ---- classify: segment tid -> slot tid+1; lanes 0..15 also one word each
+  // of the 64 bytes before the tile -> slot 0
   uint32_t bad = 0;
   {
-    const uint64_t P = t.tlo + (uint64_t)tid * kSegB;
-    const int nv = P < a.n ? (int)mn<uint64_t>(64, a.n - P) : 0;
-    const Masks m = classify64(sh.text + kPre + tid * kSegB, nv);
+    const Masks m = classify64(sh.text + kPre + tid * kSegB);
     sh.md[tid + 1] = m.d;
     sh.mn[tid + 1] = m.n;
     sh.mc[tid + 1] = m.c;
     bad = m.bad;
-    if (tid == 0) {
-      if (t.tlo > 0) {
-        const Masks p = classify64(sh.text, 64);
-        sh.md[0] = p.d;
-        sh.mn[0] = p.n;
-        sh.mc[0] = p.c;
-      } else {
-        sh.md[0] = sh.mn[0] = sh.mc[0] = 0;
-      }
-      bad |= sh.tot[4];
+    if (tid < 16 && t.tlo > 0) {
+      uint32_t x;
+      memcpy(&x, sh.text + 4 * tid, 4);
+      const Nib b = classify_dword(x);
+      atomic_or_u64(&sh.md[0], (uint64_t)b.d << (4 * tid));
+      atomic_or_u64(&sh.mn[0], (uint64_t)b.n << (4 * tid));
+      atomic_or_u64(&sh.mc[0], (uint64_t)b.c << (4 * tid));
     }
+    if (tid == 0) bad |= sh.toomany;
   }
   bk.sync();
+  FSVM_STAMP(k, 3);
   // ---- roles, counts, eligibility
   const SegOut so = segment_roles(t, tid);
-  Cnt5 mine;
-  mine.c[0] = (uint32_t)popc64(so.L);
-  mine.c[1] = (uint32_t)popc64(so.W);
-  mine.c[2] = (uint32_t)popc64(so.I);
-  mine.c[3] = (uint32_t)popc64(so.V);
-  mine.c[4] = bad | so.bad;
-  Cnt5 zero;
-  for (int i = 0; i < 5; ++i) zero.c[i] = 0;
-  Cnt5 tot;
-  const Cnt5 ex = bk.exclusive(mine, zero, Cnt5Add(), &tot);
-  // ---- run lists (tile-relative offsets), grouped by role
-  if (MODE == 2) {
-    const uint32_t bL = ex.c[0], bW = tot.c[0] + ex.c[1], bI = tot.c[0] + tot.c[1] + ex.c[2],
-                   bV = tot.c[0] + tot.c[1] + tot.c[2] + ex.c[3];
-    const uint16_t off = (uint16_t)(tid * kSegB);
-    uint64_t m;
-    uint32_t j;
-    for (m = so.L, j = bL; m; m &= m - 1) sh.runs[j++] = (uint16_t)(off + ctz64(m));
-    for (m = so.W, j = bW; m; m &= m - 1) sh.runs[j++] = (uint16_t)(off + ctz64(m));
-    for (m = so.I, j = bI; m; m &= m - 1) sh.runs[j++] = (uint16_t)(off + ctz64(m));
-    for (m = so.V, j = bV; m; m &= m - 1) sh.runs[j++] = (uint16_t)(off + ctz64(m));
-  }
-  // ---- decoupled look-back: output base of this tile per counter
+  if (so.bad | bad) atomic_or_u32(&sh.bad, 1u);
+  // per-thread role counts packed in 16-bit fields (a tile holds < 2^16 runs)
+  const uint64_t mine = (uint64_t)popc64(so.L) | ((uint64_t)popc64(so.W) << 16) |
+                        ((uint64_t)popc64(so.I) << 32) | ((uint64_t)popc64(so.V) << 48);
+  uint64_t totp;
+  const uint64_t ex = bk.exclusive(mine, (uint64_t)0, AddU64(), &totp);
+  FSVM_STAMP(k, 4);
+  const uint32_t nL = (uint32_t)(totp & 0xFFFF), nW = (uint32_t)((totp >> 16) & 0xFFFF),
+                 nI = (uint32_t)((totp >> 32) & 0xFFFF), nV = (uint32_t)(totp >> 48);
+  // ---- publish this tile's aggregate (words 0-3 of its look-back record;
+  // the inclusive prefix goes to words 4-7, so a reader never mixes the two)
   if (tid < 4) {
-    // lane -> counter: rows (L), index (I), value (V), weight (W)
-    const uint64_t agg = tid == 0 ? tot.c[0] : tid == 1 ? tot.c[2] : tid == 2 ? tot.c[3] : tot.c[1];
-    uint64_t *w = a.lb + (uint64_t)k * 4 + tid;
-    uint64_t excl = 0;
-    if (k == 0) {
-      store_agent_u64(w, kIncl | agg);
-    } else {
-      store_agent_u64(w, kAgg | agg);
-      uint64_t j = k - 1;
-      uint32_t spins = 0;
-      for (;;) {
-        const uint64_t v = load_agent_u64(a.lb + j * 4 + tid);
-        const uint64_t f = v & ~kValMask;
-        if (f == 0) {
-          if (++spins > kSpinLimit) {  // never expected: hand the input to the exact path
-            atomic_or_u32(a.gate, 2u);
-            break;
-          }
-          spin_pause();
-          continue;
-        }
-        excl += v & kValMask;
-        if (f == kIncl) break;
-        --j;
-      }
-      store_agent_u64(w, kIncl | (excl + agg));
-    }
-    sh.base[tid] = excl;
-    if (tid == 0 && tot.c[4]) atomic_or_u32(a.gate, 1u);
+    const uint64_t agg = tid == 0 ? nL : tid == 1 ? nI : tid == 2 ? nV : nW;
+    uint64_t *rec = a.lb + (uint64_t)k * 8;
+    if (k == 0) store_agent_u64(rec + 4 + tid, kIncl | agg);
+    else store_agent_u64(rec + tid, kAgg | agg);
+    if (tid == 0 && sh.bad) atomic_or_u32(a.gate, 1u);
   }
-  bk.sync();
-  const uint64_t bRows = sh.base[Q_ROWS], bIdx = sh.base[Q_INDEX], bVal = sh.base[Q_VALUE],
-                 bW = sh.base[Q_WEIGHT];
-  // ---- the last tile publishes the totals (dmlc_amd_result.count)
-  if (k + 1 == a.ntiles && tid == 0) {
-    const uint64_t rows = bRows + tot.c[0];
-    a.res[C_ROWS] = rows;
-    a.res[C_INDEX] = bIdx + tot.c[2];
-    a.res[C_VALUE] = bVal + tot.c[3];
-    a.res[C_WEIGHT] = bW + tot.c[1];
-    a.res[C_QID] = 0;
-    a.res[C_LABEL] = rows;
-    a.res[C_FIELD] = 0;
-    if (MODE == 2 && a.offset && rows < a.cap[C_ROWS] + 1) a.offset[rows] = bIdx + tot.c[2];
-  }
-  if (MODE != 2) return;
-
-  // ---- token-parallel decode + coalesced stores
-  const uint32_t nL = tot.c[0], nW = tot.c[1], nI = tot.c[2], nV = tot.c[3];
-  const uint16_t *rL = sh.runs, *rW = sh.runs + nL, *rI = rW + nW, *rV = rI + nI;
+  // ---- first decode batch into registers (gives predecessors time to publish)
+  const uint64_t P = t.tlo + (uint64_t)tid * kSegB;
   Src src;
   src.g = a.text;
   src.wbase = t.tlo >= (uint64_t)kPre ? t.tlo - kPre : 0;
   src.wend = mn<uint64_t>(t.thi + kPost, a.n);
   src.lds = sh.text + (src.wbase + kPre - t.tlo);
-  const bool simple_lim = sh.ncs == 0;  // no chunk boundary before cnext
-  for (uint32_t j = tid; j < nI; j += kThreads) {
-    const uint64_t q = t.tlo + rI[j];
-    src.lim = simple_lim ? sh.cnext : t.next_cs(q);
-    uint64_t v;
-    if (!parse_uint(src, q, a.wide != 0, &v)) {
+  const bool one_chunk = sh.ncs == 0;  // no chunk boundary before cnext
+  // the window decoders are exact when its 16 bytes belong to the run's chunk
+  auto lim_of = [&](uint64_t q) { return one_chunk ? sh.cnext : t.next_cs(q); };
+  auto dec_float = [&](uint64_t q) -> float {
+    const uint64_t lim = lim_of(q);
+    bool ok = false;
+    float v = 0.f;
+    if (q + 16 <= lim) v = wfloat(win_at(sh, t.tlo, q), &ok);
+    if (!ok) {
+      src.lim = lim;
+      uint64_t e;
+      bool nan_err = false;
+      v = parse_float(src, q, &e, &nan_err);
+    }
+    return v;
+  };
+  auto dec_index = [&](uint64_t q) -> uint64_t {
+    const uint64_t lim = lim_of(q);
+    uint64_t v = 0;
+    bool ok = false, pos = true;
+    if (q + 16 <= lim) pos = wuint(win_at(sh, t.tlo, q), a.wide != 0, &v, &ok);
+    if (!ok) {
+      src.lim = lim;
+      pos = parse_uint(src, q, a.wide != 0, &v);
+    }
+    if (!pos) {
       raise_error(a.err, E_NEG_INDEX, q);
       v = 0;
     }
     if (a.indexing_mode > 0) --v;
-    const uint64_t r = bIdx + j;
+    return v;
+  };
+#ifndef FSVM_KB
+#define FSVM_KB 4
+#endif
+  constexpr int kB = FSVM_KB;  // runs per role decoded before the look-back
+  uint64_t ib[kB > 0 ? kB : 1];
+  float vb[kB > 0 ? kB : 1];
+  uint64_t mI = so.I, mV = so.V;
+  if (MODE == 2) {
+#pragma unroll
+    for (int u = 0; u < kB; ++u) {
+      ib[u] = 0;
+      vb[u] = 0.f;
+      if (mI) {
+        ib[u] = dec_index(P + ctz64(mI));
+        mI &= mI - 1;
+      }
+      if (mV) {
+        vb[u] = dec_float(P + ctz64(mV));
+        mV &= mV - 1;
+      }
+    }
+  }
+  // ---- decoupled look-back by wave 0: lane i reads predecessor j-1-i's
+  // record; a round consumes predecessors up to the first inclusive one and
+  // stops before the first unpublished one
+  if (tid < kWave) {
+    const uint32_t lane = tid;
+    uint64_t j = k;
+    uint32_t spins = 0, rounds = 0;
+    uint64_t acc = 0;  // lane c < 4: counter c
+    bool done = k == 0;
+    while (!done) {
+      ++rounds;
+      uint64_t v0 = 0, v1 = 0, v2 = 0, v3 = 0;
+      uint32_t st = 2;  // before tile 0: an inclusive 0
+      if (lane < j) {
+        uint64_t *rec = a.lb + (j - 1 - lane) * 8;
+        // all eight words in one round trip
+        const uint64_t a0 = load_agent_u64(rec + 0), a1 = load_agent_u64(rec + 1),
+                       a2 = load_agent_u64(rec + 2), a3 = load_agent_u64(rec + 3),
+                       i0 = load_agent_u64(rec + 4), i1 = load_agent_u64(rec + 5),
+                       i2 = load_agent_u64(rec + 6), i3 = load_agent_u64(rec + 7);
+        const bool inc = (i0 & i1 & i2 & i3) >> 63;
+        v0 = inc ? i0 : a0;
+        v1 = inc ? i1 : a1;
+        v2 = inc ? i2 : a2;
+        v3 = inc ? i3 : a3;
+        st = inc ? 2 : ((a0 & a1 & a2 & a3) >> 62 ? 1 : 0);
+      }
+      const uint64_t zero = bk.ballot(st == 0), incl = bk.ballot(st == 2);
+      const uint32_t fz = zero ? (uint32_t)ctz64(zero) : 64u, fi = incl ? (uint32_t)ctz64(incl) : 64u;
+      const uint32_t take = fi < fz ? fi + 1 : fz;
+      const bool use = lane < take;
+      sh.lbw[4 * lane + 0] = use ? v0 & kValMask : 0;
+      sh.lbw[4 * lane + 1] = use ? v1 & kValMask : 0;
+      sh.lbw[4 * lane + 2] = use ? v2 & kValMask : 0;
+      sh.lbw[4 * lane + 3] = use ? v3 & kValMask : 0;
+      bk.wave_sync();
+      if (lane < 4)
+        for (uint32_t i = 0; i < take; ++i) acc += sh.lbw[4 * i + lane];
+      bk.wave_sync();
+      j -= take;
+      done = fi < fz;
+      if (!done && take == 0) {
+        if (++spins > kSpinLimit) {  // never expected: hand the input to the exact path
+          if (lane == 0) atomic_or_u32(a.gate, 2u);
+          done = true;
+        }
+        spin_pause();
+      }
+    }
+#if defined(DMLC_AMD_STAMPS) && defined(__HIP_DEVICE_COMPILE__)
+    if (lane == 0 && k < kStampTiles) g_stamps[(uint64_t)k * 8 + 7] = rounds;
+#else
+    (void)rounds;
+#endif
+    if (lane < 4) {
+      if (k > 0) {
+        const uint64_t agg = lane == 0 ? nL : lane == 1 ? nI : lane == 2 ? nV : nW;
+        store_agent_u64(a.lb + (uint64_t)k * 8 + 4 + lane, kIncl | (acc + agg));
+      }
+      sh.base[lane] = acc;
+    }
+  }
+  bk.sync();
+  FSVM_STAMP(k, 5);
+  const uint64_t bRows = sh.base[Q_ROWS], bIdx = sh.base[Q_INDEX], bVal = sh.base[Q_VALUE],
+                 bW = sh.base[Q_WEIGHT];
+  // ---- the last tile publishes the totals (dmlc_amd_result.count)
+  if (k + 1 == a.ntiles && tid == 0) {
+    const uint64_t rows = bRows + nL;
+    a.res[C_ROWS] = rows;
+    a.res[C_INDEX] = bIdx + nI;
+    a.res[C_VALUE] = bVal + nV;
+    a.res[C_WEIGHT] = bW + nW;
+    a.res[C_QID] = 0;
+    a.res[C_LABEL] = rows;
+    a.res[C_FIELD] = 0;
+    if (MODE == 2 && a.offset && rows < a.cap[C_ROWS] + 1) a.offset[rows] = bIdx + nI;
+  }
+  if (MODE != 2) return;
+
+  // ---- stores: the register batch, then the rest of this segment's runs,
+  // one role at a time (no divergence between the index and value decoders)
+  const uint64_t eL = bRows + (ex & 0xFFFF), eW = bW + ((ex >> 16) & 0xFFFF),
+                 eI = bIdx + ((ex >> 32) & 0xFFFF), eV = bVal + (ex >> 48);
+  auto put_index = [&](uint64_t r, uint64_t v, uint64_t q) {
     if (r < a.cap[C_INDEX]) {
       if (a.wide) reinterpret_cast<uint64_t *>(a.index)[r] = v;
       else reinterpret_cast<uint32_t *>(a.index)[r] = (uint32_t)v;
     } else {
       raise_error(a.err, E_CAPACITY, q);
     }
-  }
-  for (uint32_t j = tid; j < nV; j += kThreads) {
-    const uint64_t q = t.tlo + rV[j];
-    src.lim = simple_lim ? sh.cnext : t.next_cs(q);
-    uint64_t e;
-    bool nan_err = false;
-    const float v = parse_float(src, q, &e, &nan_err);
-    const uint64_t r = bVal + j;
+  };
+  auto put_value = [&](uint64_t r, float v, uint64_t q) {
     if (r < a.cap[C_VALUE]) a.value[r] = v;
     else raise_error(a.err, E_CAPACITY, q);
-  }
-  for (uint32_t j = tid; j < nL; j += kThreads) {
-    const uint64_t q = t.tlo + rL[j];
-    src.lim = simple_lim ? sh.cnext : t.next_cs(q);
-    uint64_t e;
-    bool nan_err = false;
-    const float v = parse_float(src, q, &e, &nan_err);
-    const uint64_t r = bRows + j;
-    if (r < a.cap[C_ROWS]) {
-      a.label[r] = v;
-      a.offset[r] = bIdx + lower_count(rI, nI, rL[j]);
-    } else {
-      raise_error(a.err, E_CAPACITY, q);
+  };
+  {
+    const uint32_t nIm = (uint32_t)popc64(so.I), nVm = (uint32_t)popc64(so.V);
+#pragma unroll
+    for (int u = 0; u < kB; ++u) {
+      if ((uint32_t)u < nIm) put_index(eI + u, ib[u], P);
+      if ((uint32_t)u < nVm) put_value(eV + u, vb[u], P);
+    }
+    uint64_t r = eI + kB;
+    for (; mI; mI &= mI - 1, ++r) {
+      const uint64_t q = P + ctz64(mI);
+      put_index(r, dec_index(q), q);
+    }
+    r = eV + kB;
+    for (; mV; mV &= mV - 1, ++r) {
+      const uint64_t q = P + ctz64(mV);
+      put_value(r, dec_float(q), q);
     }
   }
-  for (uint32_t j = tid; j < nW; j += kThreads) {
-    const uint64_t q = t.tlo + rW[j];
-    src.lim = simple_lim ? sh.cnext : t.next_cs(q);
-    uint64_t e;
-    bool nan_err = false;
-    const float v = parse_float(src, q, &e, &nan_err);
-    const uint64_t r = bW + j;
-    if (r < a.cap[C_WEIGHT]) a.weight[r] = v;
-    else raise_error(a.err, E_CAPACITY, q);
+  {
+    uint64_t r = eL;
+    for (uint64_t m = so.L; m; m &= m - 1, ++r) {
+      const int b = ctz64(m);
+      const uint64_t q = P + b;
+      const float v = dec_float(q);
+      if (r < a.cap[C_ROWS]) {
+        a.label[r] = v;
+        a.offset[r] = eI + popc64(so.I & ((1ull << b) - 1));
+      } else {
+        raise_error(a.err, E_CAPACITY, q);
+      }
+    }
   }
-  // ---- per-chunk exclusive counts at each chunk start inside the tile
+  {
+    uint64_t r = eW;
+    for (uint64_t m = so.W; m; m &= m - 1, ++r) {
+      const uint64_t q = P + ctz64(m);
+      const float v = dec_float(q);
+      if (r < a.cap[C_WEIGHT]) a.weight[r] = v;
+      else raise_error(a.err, E_CAPACITY, q);
+    }
+  }
+  FSVM_STAMP(k, 6);
+  // ---- per-chunk exclusive counts at each chunk start in my segment
   if (a.chunk_tab) {
-    for (uint32_t i = tid; i < sh.ncs; i += kThreads) {
+    for (uint32_t i = 0; i < sh.ncs; ++i) {
       const uint64_t x = sh.csl[i];
-      if (x >= t.thi) continue;
-      const uint32_t rel = (uint32_t)(x - t.tlo);
+      if (x < P || x >= P + kSegB || x >= t.thi) continue;
+      const uint64_t below = (1ull << (x - P)) - 1;
       uint64_t *row = a.chunk_tab + (uint64_t)(sh.c_first + i) * 8;
-      const uint64_t rows = bRows + lower_count(rL, nL, rel);
+      const uint64_t rows = eL + popc64(so.L & below);
       row[C_ROWS] = rows;
-      row[C_INDEX] = bIdx + lower_count(rI, nI, rel);
-      row[C_VALUE] = bVal + lower_count(rV, nV, rel);
-      row[C_WEIGHT] = bW + lower_count(rW, nW, rel);
+      row[C_INDEX] = eI + popc64(so.I & below);
+      row[C_VALUE] = eV + popc64(so.V & below);
+      row[C_WEIGHT] = eW + popc64(so.W & below);
       row[C_QID] = 0;
       row[C_LABEL] = rows;
       row[C_FIELD] = 0;

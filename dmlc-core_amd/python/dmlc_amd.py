@@ -11,7 +11,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libdmlc_amd.so")
+LIB_PATH = os.environ.get("DMLC_AMD_LIB") or os.path.join(os.path.dirname(_HERE), "lib", "libdmlc_amd.so")
 
 LIBSVM, CSV, LIBFM = 0, 1, 2
 F32, I32, I64 = 0, 1, 2
@@ -48,6 +48,13 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise RuntimeError("libdmlc_amd.so not built: run `make -C dmlc-core_amd` "
                                "(or __graft_entry__.build())")
+        # One HIP runtime per process: PyTorch ships its own libamdhip64; load
+        # it first so this library binds to the same runtime (loaded the other
+        # way round, two runtimes coexist and the second sees no device).
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB_PATH)
         L.dmlc_amd_workspace_bytes.restype = ctypes.c_size_t
         L.dmlc_amd_workspace_bytes.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(Params)]
@@ -63,6 +70,7 @@ def lib():
         L.dmlc_amd_strtof_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                             ctypes.c_void_p]
+        L.dmlc_amd_last_hip_error.restype = ctypes.c_char_p
         L.dmlc_amd_profile_begin.restype = ctypes.c_int
         L.dmlc_amd_profile_end.restype = ctypes.c_int
         L.dmlc_amd_profile_end.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int),
@@ -85,7 +93,7 @@ def profile_end():
 
 EXPORTED_SYMBOLS = ("dmlc_amd_parse", "dmlc_amd_workspace_bytes", "dmlc_amd_error_string",
                     "dmlc_amd_device_count", "dmlc_amd_abi_version", "dmlc_amd_strtof_batch",
-                    "dmlc_amd_profile_begin", "dmlc_amd_profile_end")
+                    "dmlc_amd_profile_begin", "dmlc_amd_profile_end", "dmlc_amd_last_hip_error")
 
 
 def make_params(fmt="libsvm", index_bits=32, value_type="f32", indexing_mode=0, label_column=-1,
@@ -143,7 +151,10 @@ class DeviceParser:
                                   chunk_table.data_ptr() if chunk_table is not None else None,
                                   ws.data_ptr(), ws.numel(), result.data_ptr(), s.cuda_stream)
         if rc != 0:
-            raise RuntimeError("dmlc_amd_parse: %s" % lib().dmlc_amd_error_string(rc).decode())
+            msg = lib().dmlc_amd_error_string(rc).decode()
+            if rc == 33:
+                msg += " (%s)" % lib().dmlc_amd_last_hip_error().decode()
+            raise RuntimeError("dmlc_amd_parse: %s" % msg)
 
     def count(self, text, chunk_starts, stream=None, result=None):
         """Size query: exact per-slot totals (device work, then a host sync).

@@ -135,6 +135,9 @@ int dmlc_amd_profile_end(double *total_ms, int *launches, const char **kernel);
 /* Human-readable message for an error code (matches the reference's CHECK text). */
 const char *dmlc_amd_error_string(int code);
 
+/* hipGetErrorString of the HIP error behind this thread's last DMLC_AMD_ERR_HIP. */
+const char *dmlc_amd_last_hip_error(void);
+
 /* Number of visible HIP devices (0 when no GPU / no driver). */
 int dmlc_amd_device_count(void);
 

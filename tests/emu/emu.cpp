@@ -42,6 +42,8 @@ struct Barrier {
 
 struct BlockCtx {
   Barrier bar{kThreads};
+  Barrier wbar[kWaves] = {Barrier(kWave), Barrier(kWave), Barrier(kWave), Barrier(kWave)};
+  unsigned char bal[kThreads];
   alignas(64) unsigned char scan[kThreads * 64];
   uint64_t mins[kThreads];
 };
@@ -51,6 +53,16 @@ struct HostBlock {
   BlockCtx *ctx;
   int tid() const { return t; }
   void sync() { ctx->bar.wait(); }
+  void wave_sync() { ctx->wbar[t / kWave].wait(); }
+  uint64_t ballot(bool p) {
+    ctx->bal[t] = p;
+    wave_sync();
+    uint64_t m = 0;
+    const int w0 = t / kWave * kWave;
+    for (int i = 0; i < kWave; ++i) m |= (uint64_t)(ctx->bal[w0 + i] != 0) << i;
+    wave_sync();
+    return m;
+  }
   uint64_t min_u64(uint64_t v) {
     ctx->mins[t] = v;
     sync();
@@ -119,7 +131,7 @@ extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *c
     const uint64_t nft = (nbytes + fsvm::kTile - 1) / fsvm::kTile;
     uint32_t gate = use_fast ? 0u : 1u, ticket = 0;
     unsigned long long ferr = ~0ull;
-    std::vector<uint64_t> lb(nft * 4 + 1, 0);
+    std::vector<uint64_t> lb(nft * 8 + 1, 0);
     LibsvmArgs a;
     std::memset(&a, 0, sizeof(a));
     a.text = text;

@@ -1,0 +1,67 @@
+"""Phase breakdown of the single-pass libsvm kernel (diagnostic build).
+
+Loads dmlc-core_amd/lib/libdmlc_amd_stamps.so (make -C dmlc-core_amd stamps),
+parses a synthetic shard, and prints the mean shader cycles each tile spends
+per phase: 1->2 staging, 2->3 classify, 3->4 roles + block scan,
+4->5 look-back, 5->6 decode + stores.  Stamp values never feed an output.
+"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "dmlc-core_amd", "python")]
+
+import dmlc_amd  # noqa: E402
+from tools import synth  # noqa: E402
+
+PHASES = ["stage", "classify", "roles+scan", "look-back", "decode+store"]
+
+
+def main():
+    rows = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 20
+    width = int(sys.argv[2]) if len(sys.argv) > 2 else 128
+    dmlc_amd.LIB_PATH = os.path.join(ROOT, "dmlc-core_amd", "lib", "libdmlc_amd_stamps.so")
+    L = dmlc_amd.lib()
+    L.dmlc_amd_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+    import torch
+    text, _ = synth.rows(synth.LIBSVM, rows, width, seed=1)
+    starts = dmlc_amd.text_chunk_starts(text)
+    d_text = torch.from_numpy(text).cuda()
+    d_cs = torch.from_numpy(starts).cuda()
+    p = dmlc_amd.DeviceParser("libsvm")
+    res = torch.zeros(16, dtype=torch.int64, device="cuda")
+    counts = p.count(d_text, d_cs, result=res)
+    out = p.alloc(counts)
+    out["_csr"] = p.csr_of(out)
+    ntiles = (text.size + 16383) // 16384
+    n = min(ntiles, 1 << 17)
+    for mode in ("count", "full"):
+        for _ in range(3):
+            if mode == "count":
+                p.count_async(d_text, d_cs, res)
+            else:
+                p.parse_into(d_text, d_cs, out, res)
+        torch.cuda.synchronize()
+        st = np.zeros(n * 8, dtype=np.uint64)
+        assert L.dmlc_amd_debug_stamps(st.ctypes.data, st.nbytes) == 0
+        st = st.reshape(n, 8).astype(np.int64)
+        last = 6 if mode == "full" else 5
+        d = np.diff(st[:, 1:last + 1], axis=1)
+        rt = st[:, 0]
+        print("%s: %d tiles, wall span of tile starts %.3f ms (100 MHz clock)"
+              % (mode, n, (rt.max() - rt.min()) / 1e5))
+        for i in range(d.shape[1]):
+            col = d[:, i]
+            print("  %-14s mean %8.0f cyc  p50 %8.0f  p99 %8.0f" % (PHASES[i], col.mean(), np.median(col),
+                                                                   np.percentile(col, 99)))
+        print("  total          mean %8.0f cyc" % d.sum(axis=1).mean())
+        rounds = st[:, 7]
+        print("  look-back rounds: mean %.2f p50 %.0f p99 %.0f max %d"
+              % (rounds.mean(), np.median(rounds), np.percentile(rounds, 99), rounds.max()))
+
+
+if __name__ == "__main__":
+    main()
