@@ -108,7 +108,7 @@ hipError_t launch_libsvm(const LibsvmArgs &a, const FastSvmArgs &f, bool use_fas
 #if defined(DMLC_AMD_STAMPS)
 // diagnostic build: copy the phase stamps of the last launch to the host
 extern "C" int dmlc_amd_debug_stamps(void *dst, size_t bytes) {
-  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(dmlc_amd::fsvm::g_stamps), bytes, 0,
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(dmlc_amd::fast::g_stamps), bytes, 0,
                              hipMemcpyDeviceToHost) == hipSuccess ? 0 : 33;
 }
 #endif

@@ -23,300 +23,23 @@
 // Written once against a block policy BK {tid, sync, exclusive} so the GPU
 // kernel (libsvm.hip) and the test-only CPU emulator (tests/emu) share it.
 #pragma once
-#include "args.h"
-#include "decode.h"
+#include "fast_common.h"
 
 namespace dmlc_amd {
 namespace fsvm {
-
-constexpr int kSegB = 64;                // bytes per thread (one 64-bit mask)
-constexpr int kTile = kThreads * kSegB;  // 16 KiB of text per tile
-constexpr int kPre = 64;                 // staged bytes before the tile (look-back)
-constexpr int kPost = 128;               // staged bytes after it (runs crossing the end)
-constexpr int kStage = kPre + kTile + kPost;
-constexpr int kMaxCs = 32;               // chunk starts per tile the fast path accepts
-constexpr uint64_t kAgg = 1ull << 62, kIncl = 2ull << 62, kValMask = (1ull << 62) - 1;
-constexpr uint32_t kSpinLimit = 1u << 26;
+using namespace fast;
 
 enum : uint32_t { R_NONE = 0, R_L = 1, R_K = 2, R_I = 3 };
 
-// Diagnostic build only (-DDMLC_AMD_STAMPS, libdmlc_amd_stamps.so): thread 0
-// of each tile records s_memtime at phase boundaries into g_stamps; the
-// product build executes no stamp.
-constexpr uint32_t kStampTiles = 1u << 17;
-#if defined(DMLC_AMD_STAMPS) && defined(__HIPCC__)
-__device__ uint64_t g_stamps[kStampTiles * 8];
-#endif
-#if defined(DMLC_AMD_STAMPS) && defined(__HIP_DEVICE_COMPILE__)
-#define FSVM_STAMP(k, i)                                                         \
-  do {                                                                           \
-    if (tid == 0 && (k) < kStampTiles) {                                         \
-      __builtin_amdgcn_sched_barrier(0);                                         \
-      g_stamps[(uint64_t)(k) * 8 + (i)] =                                        \
-          (i) == 0 ? __builtin_amdgcn_s_memrealtime() : __builtin_amdgcn_s_memtime(); \
-      __builtin_amdgcn_sched_barrier(0);                                         \
-    }                                                                            \
-  } while (0)
-#else
-#define FSVM_STAMP(k, i) \
-  do {                   \
-  } while (0)
-#endif
 // look-back counter slots (record words 0-3: aggregate, 4-7: inclusive prefix)
 enum { Q_ROWS = 0, Q_INDEX = 1, Q_VALUE = 2, Q_WEIGHT = 3 };
 
-// Byte classes by two 16-entry nibble tables (v_perm_b32 lookups): cls =
-// LO[b & 15] & HI[b >> 4]; bits 0-2 digitchar (strtonum.h:70-72: 0-9, then
-// + - ., then e E), bit 3 ':', bit 4 '\n' '\r', bits 5-6 ' ' '\t'
-// (strtonum.h:37-39).  A zero class is a byte outside the grammar.
-constexpr uint32_t kLoA = 0x01010121u, kLoB = 0x01010501u;  // LO[0..7]
-constexpr uint32_t kLoC = 0x02184101u, kLoD = 0x00021200u;  // LO[8..15]
-constexpr uint32_t kHiA = 0x09220050u, kHiB = 0x00040004u;  // HI[0..7]
-
-struct Masks {
-  uint64_t d, n, c;
-  uint32_t bad;
-};
-
-DA_HD uint32_t nib_d(uint32_t cls) {  // digitchar byte flags -> 4 bits
-  return ((((cls & 0x07070707u) + 0x7F7F7F7Fu) & 0x80808080u) * 0x00204081u) >> 28;
-}
-DA_HD uint32_t nib_n(uint32_t cls) { return ((cls & 0x10101010u) * 0x01020408u) >> 28; }
-DA_HD uint32_t nib_c(uint32_t cls) { return ((cls & 0x08080808u) * 0x02040810u) >> 28; }
-
-DA_HD uint32_t classify4(uint32_t x) {
-  const uint32_t lo = x & 0x0F0F0F0Fu, s = lo & 0x07070707u;
-  const uint32_t a = perm_b32(kLoB, kLoA, s), b = perm_b32(kLoD, kLoC, s);
-  const uint32_t m8 = ((lo >> 3) & 0x01010101u) * 0xFFu;
-  const uint32_t lov = (b & m8) | (a & ~m8);
-  const uint32_t hv = perm_b32(kHiB, kHiA, (x >> 4) & 0x07070707u);
-  return lov & hv;
-}
-
-DA_HD void load16(const uint8_t *p, uint32_t w[4]) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  const uint4 v = *reinterpret_cast<const uint4 *>(p);
-  w[0] = v.x;
-  w[1] = v.y;
-  w[2] = v.z;
-  w[3] = v.w;
-#else
-  memcpy(w, p, 16);
-#endif
-}
-
-struct Nib {
-  uint32_t d, n, c, bad;
-};
-DA_HD Nib classify_dword(uint32_t x) {  // 4-bit masks of 4 bytes; bad: a byte outside the grammar
-  const uint32_t cls = classify4(x);
-  Nib r;
-  r.d = nib_d(cls);
-  r.n = nib_n(cls);
-  r.c = nib_c(cls);
-  r.bad = ((cls + 0x7F7F7F7Fu) & 0x80808080u) != 0x80808080u || (x & 0x80808080u);
-  return r;
-}
-
-// Masks of the 64 bytes at p (16-byte aligned).  Bytes past the end of the
-// text are staged as blanks, so they are neutral here.
-DA_HD Masks classify64(const uint8_t *p) {
-  uint32_t dl = 0, dh = 0, nl = 0, nh = 0, cl = 0, ch = 0;
-  uint32_t all = 0x80808080u, orv = 0;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    uint32_t w[4];
-    load16(p + 16 * q, w);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int i = 4 * q + j;
-      const uint32_t x = w[j];
-      const uint32_t cls = classify4(x);
-      all &= cls + 0x7F7F7F7Fu;
-      orv |= x;
-      const int sh = 4 * (i & 7);
-      if (i < 8) {
-        dl |= nib_d(cls) << sh;
-        nl |= nib_n(cls) << sh;
-        cl |= nib_c(cls) << sh;
-      } else {
-        dh |= nib_d(cls) << sh;
-        nh |= nib_n(cls) << sh;
-        ch |= nib_c(cls) << sh;
-      }
-    }
-  }
-  Masks m;
-  m.d = dl | ((uint64_t)dh << 32);
-  m.n = nl | ((uint64_t)nh << 32);
-  m.c = cl | ((uint64_t)ch << 32);
-  m.bad = ((all & 0x80808080u) != 0x80808080u) || (orv & 0x80808080u);
-  return m;
-}
-
 struct Shared {  // LDS of one workgroup
-  alignas(16) uint8_t text[kStage];               // position p <-> text[p - tlo + kPre]
-  uint64_t md[kThreads + 1];          // slot 0: the segment before the tile; slot t+1: segment t
+  TileCommon c;
+  uint64_t md[kThreads + 1];  // slot 0: the segment before the tile; slot t+1: segment t
   uint64_t mn[kThreads + 1];
   uint64_t mc[kThreads + 1];
-  uint64_t csl[kMaxCs + 1];           // chunk starts in [tlo, thi]
-  uint64_t cfloor, cnext, base[4];
-  uint64_t lbw[4 * kWave];            // look-back round: values per lane and counter
-  uint32_t ncs, c_first, tile, toomany, bad;
 };
-
-struct AddU64 {
-  DA_HD uint64_t operator()(uint64_t a, uint64_t b) const { return a + b; }
-};
-
-// ---- SWAR decoders on the first 16 bytes of a run (read from the staged LDS
-// text with five aligned words).  Digits are located with byte-parallel masks
-// and converted eight at a time (multiply-shift 8-digit conversion), then
-// combined with exactly the reference's arithmetic.
-
-DA_HD uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t sft) {  // ((hi:lo) >> sft), sft < 32
-#if defined(__HIP_DEVICE_COMPILE__)
-  return __builtin_amdgcn_alignbit(hi, lo, sft);
-#else
-  return (uint32_t)((((uint64_t)hi << 32) | lo) >> sft);
-#endif
-}
-
-DA_HD uint32_t nondigit8(uint64_t x) {  // bit i: byte i is not '0'..'9' (grammar bytes < 0x80)
-  const uint64_t t = x ^ 0x3030303030303030ull;
-  const uint64_t h = ((t + 0x7676767676767676ull) & 0x8080808080808080ull) >> 7;
-  return (uint32_t)((h * 0x0102040810204080ull) >> 56);
-}
-
-DA_HD uint64_t parse8(uint64_t w) {  // 8 ASCII digits, first char in the low byte
-  w = ((w & 0x0F0F0F0F0F0F0F0Full) * 2561ull) >> 8;
-  w = ((w & 0x00FF00FF00FF00FFull) * 6553601ull) >> 16;
-  return ((w & 0x0000FFFF0000FFFFull) * 42949672960001ull) >> 32;
-}
-
-struct W16 {
-  uint64_t lo, hi;  // window bytes 0..7, 8..15
-  DA_HD uint32_t byte(uint32_t p) const {
-    return (uint32_t)((p < 8 ? lo >> (8 * p) : hi >> (8 * (p - 8))) & 0xFFu);
-  }
-  DA_HD uint64_t at(uint32_t a) const {  // bytes a .. a+7 (zero beyond the window)
-    if (a == 0) return lo;
-    if (a < 8) return (lo >> (8 * a)) | (hi << (64 - 8 * a));
-    return a < 16 ? hi >> (8 * (a - 8)) : 0;
-  }
-  DA_HD uint64_t span8(uint32_t a, uint32_t len) const {  // value of len <= 8 digits at a
-    if (len == 0) return 0;
-    uint64_t w = at(a) << (8 * (8 - len));
-    if (len < 8) w |= 0x3030303030303030ull >> (8 * len);
-    return parse8(w);
-  }
-  DA_HD uint64_t span16(uint32_t a, uint32_t len) const {  // len <= 16
-    return len <= 8 ? span8(a, len) : span8(a, len - 8) * 100000000ull + span8(a + len - 8, 8);
-  }
-  DA_HD uint32_t digits() const { return ~(nondigit8(lo) | (nondigit8(hi) << 8)) & 0xFFFFu; }
-};
-
-DA_HD uint32_t run_len(uint32_t dm, uint32_t a) {  // consecutive digits from byte a
-  return a >= 16 ? 0 : (uint32_t)ctz32(~(dm >> a));
-}
-
-DA_HD double pow10_exact(uint32_t k) {  // 10^k as a double, exact for k <= 22
-  double p = 1.0;
-  if (k & 1u) p *= 10.0;
-  if (k & 2u) p *= 100.0;
-  if (k & 4u) p *= 1e4;
-  if (k & 8u) p *= 1e8;
-  if (k & 16u) p *= 1e16;
-  return p;
-}
-
-// ParseFloat<float> (strtonum.h:95-264) restated for a run of the uniform
-// grammar -- inf / nan / the 'f' suffix need letters outside it -- with the
-// reference's operations: u64 integer part, f32 conversion, one f64 division
-// of the (<= 19-digit) fraction, f32 add, f32 exponent scaling.
-// *ok = false when the number may continue past the window (caller falls back).
-DA_HD float wfloat(const W16 &w, bool *ok) {
-  const uint32_t dm = w.digits();
-  const uint32_t b0 = w.byte(0);
-  const bool sign = b0 != '-';
-  const uint32_t s = (b0 == '-' || b0 == '+') ? 1u : 0u;
-  const uint32_t il = run_len(dm, s);
-  uint32_t p = s + il;
-  *ok = false;
-  if (p >= 16) return 0.f;
-  float value = (float)w.span16(s, il);
-  uint32_t c = w.byte(p);
-  if (c == '.') {
-    const uint32_t fs = p + 1;
-    const uint32_t fl = run_len(dm, fs);
-    p = fs + fl;
-    if (p >= 16) return 0.f;
-    value += (float)((double)w.span16(fs, fl) / pow10_exact(fl));
-    c = w.byte(p);
-  }
-  if (c == 'e' || c == 'E') {
-    bool frac = false;
-    float scale = 1.0f;
-    if (++p >= 16) return 0.f;
-    c = w.byte(p);
-    if (c == '-' || c == '+') {
-      frac = c == '-';
-      if (++p >= 16) return 0.f;
-      c = w.byte(p);
-    }
-    uint32_t expon = 0;
-    for (; is_digit(c); c = w.byte(p)) {
-      expon = expon * 10u + (c - '0');
-      if (++p >= 16) return 0.f;
-    }
-    if (expon > 38u) expon = 38u;
-    const float kMaxSig = (float)3.402823466, kMaxSigNeg = (float)1.175494351;
-    if (expon == 38u && ((!frac && value > kMaxSig) || (frac && value < kMaxSigNeg)))
-      value = frac ? kMaxSigNeg : kMaxSig;
-    while (expon >= 8u) {
-      scale *= 1E8f;
-      expon -= 8u;
-    }
-    while (expon > 0u) {
-      scale *= 10.0f;
-      expon -= 1u;
-    }
-    value = frac ? (value / scale) : (value * scale);
-  }
-  *ok = true;
-  return sign ? value : -value;
-}
-
-// ParseUnsignedInt (strtonum.h:392-428) on a run (no leading blanks there):
-// false on a leading '-' (the reference's fatal CHECK).  Up to 16 digits the
-// exact value truncated to the index width equals the reference's wrapping
-// accumulation.
-DA_HD bool wuint(const W16 &w, bool wide, uint64_t *out, bool *ok) {
-  const uint32_t b0 = w.byte(0);
-  *ok = true;
-  if (b0 == '-') return false;
-  const uint32_t s = b0 == '+' ? 1u : 0u;
-  const uint32_t il = run_len(w.digits(), s);
-  if (s + il >= 16) {
-    *ok = false;
-    return true;
-  }
-  const uint64_t v = w.span16(s, il);
-  *out = wide ? v : (uint64_t)(uint32_t)v;
-  return true;
-}
-
-// the 16 bytes at absolute position q (staged in LDS; q < thi) as a window
-DA_HD W16 win_at(const Shared &sh, uint64_t tlo, uint64_t q) {
-  const uint32_t off = (uint32_t)(q - tlo) + kPre;
-  const uint32_t *w = reinterpret_cast<const uint32_t *>(sh.text + (off & ~3u));
-  const uint32_t sft = (off & 3u) * 8u;
-  const uint32_t x0 = w[0], x1 = w[1], x2 = w[2], x3 = w[3], x4 = w[4];
-  W16 r;
-  r.lo = funnel(x1, x0, sft) | ((uint64_t)funnel(x2, x1, sft) << 32);
-  r.hi = funnel(x3, x2, sft) | ((uint64_t)funnel(x4, x3, sft) << 32);
-  return r;
-}
 
 struct Tile {
   const FastSvmArgs *a;
@@ -333,10 +56,20 @@ struct Tile {
       *c = sh->mc[s];
       return;
     }
-    const Masks m = classify64(a->text + (g << 6));
-    *d = m.d;
-    *n = m.n;
-    *c = m.c;
+    // beyond the staged bytes (a gap or run longer than the pre-halo): a
+    // compact byte loop, kept out of line of the register budget
+    uint64_t md = 0, mn = 0, mc = 0;
+    const uint8_t *p = a->text + (g << 6);
+#pragma unroll 1
+    for (int i = 0; i < 64; ++i) {
+      const uint32_t b = p[i];
+      md |= (uint64_t)is_digitchar(b) << i;
+      mn |= (uint64_t)is_nl(b) << i;
+      mc |= (uint64_t)(b == ':') << i;
+    }
+    *d = md;
+    *n = mn;
+    *c = mc;
   }
 
   // last position in [lo, hi) whose bit is set in mask `kind` (0 D, 1 not-D,
@@ -356,19 +89,19 @@ struct Tile {
   }
 
   DA_HD uint64_t floor_of(uint64_t p) const {  // last chunk start <= p
-    uint64_t f = sh->cfloor;
-    for (uint32_t i = 0; i < sh->ncs && sh->csl[i] <= p; ++i) f = sh->csl[i];
+    uint64_t f = sh->c.cfloor;
+    for (uint32_t i = 0; i < sh->c.ncs && sh->c.csl[i] <= p; ++i) f = sh->c.csl[i];
     return f;
   }
   DA_HD uint64_t next_cs(uint64_t p) const {  // first chunk start > p
-    for (uint32_t i = 0; i < sh->ncs; ++i)
-      if (sh->csl[i] > p) return sh->csl[i];
-    return sh->cnext;
+    for (uint32_t i = 0; i < sh->c.ncs; ++i)
+      if (sh->c.csl[i] > p) return sh->c.csl[i];
+    return sh->c.cnext;
   }
   DA_HD bool is_cs(uint64_t p) const {
-    for (uint32_t i = 0; i < sh->ncs; ++i)
-      if (sh->csl[i] == p) return true;
-    return p == sh->cnext;
+    for (uint32_t i = 0; i < sh->c.ncs; ++i)
+      if (sh->c.csl[i] == p) return true;
+    return p == sh->c.cnext;
   }
 
   // role of the run starting at q (q > its chunk start f, or == f)
@@ -434,8 +167,8 @@ DA_HD SegOut segment_roles(const Tile &t, int tid) {
   const uint64_t valid = nv == 64 ? ~0ull : ((1ull << nv) - 1);
   const uint64_t D = t.sh->md[tid + 1], N = t.sh->mn[tid + 1], C = t.sh->mc[tid + 1];
   uint64_t S = 0;
-  for (uint32_t i = 0; i < t.sh->ncs; ++i) {
-    const uint64_t x = t.sh->csl[i];
+  for (uint32_t i = 0; i < t.sh->c.ncs; ++i) {
+    const uint64_t x = t.sh->c.csl[i];
     if (x >= P && x < P + (uint64_t)nv) S |= 1ull << (x - P);
   }
   // ---- carry-in: state just before P
@@ -494,108 +227,60 @@ DA_HD SegOut segment_roles(const Tile &t, int tid) {
 template <int MODE, class BK>
 DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk) {
   const int tid = bk.tid();
-  if (tid == 0) {
-    sh.tile = (a.skip_if_gated && *a.gate) ? ~0u : atomic_add_u32(a.ticket, 1);
-  }
+  if (tid == 0) sh.c.tile = (a.skip_if_gated && *a.gate) ? ~0u : atomic_add_u32(a.ticket, 1);
   bk.sync();
-  const uint32_t k = sh.tile;
+  const uint32_t k = sh.c.tile;
   if (k == ~0u) return;
-  FSVM_STAMP(k, 0);
-  FSVM_STAMP(k, 1);
+  FAST_STAMP(k, 0);
+  FAST_STAMP(k, 1);
   Tile t;
   t.a = &a;
   t.sh = &sh;
   t.tlo = (uint64_t)k * kTile;
   t.thi = mn<uint64_t>(t.tlo + kTile, a.n);
-
-  // ---- chunk starts touching the tile (binary search once)
   if (tid == 0) {
-    const int c0 = chunk_of(a.cs, a.nchunk, t.tlo);
-    sh.cfloor = a.cs[c0];
-    int c = c0;
-    if (a.cs[c] < t.tlo) ++c;
-    sh.c_first = (uint32_t)c;
-    uint32_t m = 0;
-    while (c < a.nchunk && a.cs[c] <= t.thi) {
-      if (m < kMaxCs) sh.csl[m] = a.cs[c];
-      ++m;
-      ++c;
-    }
-    sh.ncs = m < kMaxCs ? m : kMaxCs;
-    sh.cnext = a.cs[c];  // cs[nchunk] == n
-    sh.toomany = m > kMaxCs;
-    sh.bad = 0;
+    chunk_list(a.cs, a.nchunk, t.tlo, t.thi, sh.c);
     sh.md[0] = sh.mn[0] = sh.mc[0] = 0;
   }
-  // ---- stage [tlo - kPre, tlo + kTile + kPost) into LDS; bytes past the end
-  // of the text become blanks (neutral to the classifier; never decoded)
-  {
-    const uint64_t s0 = t.tlo >= (uint64_t)kPre ? t.tlo - kPre : 0;
-    const uint64_t s1 = t.tlo + kTile + kPost;
-    uint8_t *dst = sh.text + (s0 + kPre - t.tlo);
-    const uint64_t nunits = (s1 - s0) >> 4;
-    for (uint64_t u = tid; u < nunits; u += kThreads) {
-      const uint64_t g = s0 + (u << 4);
-      uint32_t w[4];
-      if (g + 16 <= a.n) {
-        load16(a.text + g, w);
-      } else {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          uint32_t x = 0;
-#pragma unroll
-          for (int b = 0; b < 4; ++b) {
-            const uint64_t pos = g + 4 * q + b;
-            x |= (uint32_t)(pos < a.n ? a.text[pos] : (uint8_t)' ') << (8 * b);
-          }
-          w[q] = x;
-        }
-      }
-      memcpy(dst + (u << 4), w, 16);
-    }
-  }
+  stage(a.text, a.n, t.tlo, sh.c, bk);
   bk.sync();
-  FSVM_STAMP(k, 2);
+  FAST_STAMP(k, 2);
   // ---- classify: segment tid -> slot tid+1; lanes 0..15 also one word each
   // of the 64 bytes before the tile -> slot 0
   uint32_t bad = 0;
   {
-    const Masks m = classify64(sh.text + kPre + tid * kSegB);
+    const Masks m = classify64(sh.c.text + kPre + tid * kSegB);
     sh.md[tid + 1] = m.d;
     sh.mn[tid + 1] = m.n;
     sh.mc[tid + 1] = m.c;
     bad = m.bad;
     if (tid < 16 && t.tlo > 0) {
       uint32_t x;
-      memcpy(&x, sh.text + 4 * tid, 4);
+      memcpy(&x, sh.c.text + 4 * tid, 4);
       const Nib b = classify_dword(x);
       atomic_or_u64(&sh.md[0], (uint64_t)b.d << (4 * tid));
       atomic_or_u64(&sh.mn[0], (uint64_t)b.n << (4 * tid));
       atomic_or_u64(&sh.mc[0], (uint64_t)b.c << (4 * tid));
     }
-    if (tid == 0) bad |= sh.toomany;
+    if (tid == 0) bad |= sh.c.toomany;
   }
   bk.sync();
-  FSVM_STAMP(k, 3);
+  FAST_STAMP(k, 3);
   // ---- roles, counts, eligibility
   const SegOut so = segment_roles(t, tid);
-  if (so.bad | bad) atomic_or_u32(&sh.bad, 1u);
+  if (so.bad | bad) atomic_or_u32(&sh.c.bad, 1u);
   // per-thread role counts packed in 16-bit fields (a tile holds < 2^16 runs)
   const uint64_t mine = (uint64_t)popc64(so.L) | ((uint64_t)popc64(so.W) << 16) |
                         ((uint64_t)popc64(so.I) << 32) | ((uint64_t)popc64(so.V) << 48);
   uint64_t totp;
   const uint64_t ex = bk.exclusive(mine, (uint64_t)0, AddU64(), &totp);
-  FSVM_STAMP(k, 4);
+  FAST_STAMP(k, 4);
   const uint32_t nL = (uint32_t)(totp & 0xFFFF), nW = (uint32_t)((totp >> 16) & 0xFFFF),
                  nI = (uint32_t)((totp >> 32) & 0xFFFF), nV = (uint32_t)(totp >> 48);
-  // ---- publish this tile's aggregate (words 0-3 of its look-back record;
-  // the inclusive prefix goes to words 4-7, so a reader never mixes the two)
+  // ---- publish this tile's aggregate
   if (tid < 4) {
-    const uint64_t agg = tid == 0 ? nL : tid == 1 ? nI : tid == 2 ? nV : nW;
-    uint64_t *rec = a.lb + (uint64_t)k * 8;
-    if (k == 0) store_agent_u64(rec + 4 + tid, kIncl | agg);
-    else store_agent_u64(rec + tid, kAgg | agg);
-    if (tid == 0 && sh.bad) atomic_or_u32(a.gate, 1u);
+    publish_aggregate(a.lb, k, tid, tid == 0 ? nL : tid == 1 ? nI : tid == 2 ? nV : nW);
+    if (tid == 0 && sh.c.bad) atomic_or_u32(a.gate, 1u);
   }
   // ---- first decode batch into registers (gives predecessors time to publish)
   const uint64_t P = t.tlo + (uint64_t)tid * kSegB;
@@ -603,15 +288,15 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk) {
   src.g = a.text;
   src.wbase = t.tlo >= (uint64_t)kPre ? t.tlo - kPre : 0;
   src.wend = mn<uint64_t>(t.thi + kPost, a.n);
-  src.lds = sh.text + (src.wbase + kPre - t.tlo);
-  const bool one_chunk = sh.ncs == 0;  // no chunk boundary before cnext
+  src.lds = sh.c.text + (src.wbase + kPre - t.tlo);
+  const bool one_chunk = sh.c.ncs == 0;  // no chunk boundary before cnext
   // the window decoders are exact when its 16 bytes belong to the run's chunk
-  auto lim_of = [&](uint64_t q) { return one_chunk ? sh.cnext : t.next_cs(q); };
+  auto lim_of = [&](uint64_t q) { return one_chunk ? sh.c.cnext : t.next_cs(q); };
   auto dec_float = [&](uint64_t q) -> float {
     const uint64_t lim = lim_of(q);
     bool ok = false;
     float v = 0.f;
-    if (q + 16 <= lim) v = wfloat(win_at(sh, t.tlo, q), &ok);
+    if (q + 16 <= lim) v = wfloat(win_at(sh.c.text, t.tlo, q), &ok);
     if (!ok) {
       src.lim = lim;
       uint64_t e;
@@ -624,7 +309,7 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk) {
     const uint64_t lim = lim_of(q);
     uint64_t v = 0;
     bool ok = false, pos = true;
-    if (q + 16 <= lim) pos = wuint(win_at(sh, t.tlo, q), a.wide != 0, &v, &ok);
+    if (q + 16 <= lim) pos = wuint(win_at(sh.c.text, t.tlo, q), a.wide != 0, &v, &ok);
     if (!ok) {
       src.lim = lim;
       pos = parse_uint(src, q, a.wide != 0, &v);
@@ -658,72 +343,20 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk) {
       }
     }
   }
-  // ---- decoupled look-back by wave 0: lane i reads predecessor j-1-i's
-  // record; a round consumes predecessors up to the first inclusive one and
-  // stops before the first unpublished one
+  // ---- decoupled look-back by wave 0 (fast_common.h)
   if (tid < kWave) {
-    const uint32_t lane = tid;
-    uint64_t j = k;
-    uint32_t spins = 0, rounds = 0;
-    uint64_t acc = 0;  // lane c < 4: counter c
-    bool done = k == 0;
-    while (!done) {
-      ++rounds;
-      uint64_t v0 = 0, v1 = 0, v2 = 0, v3 = 0;
-      uint32_t st = 2;  // before tile 0: an inclusive 0
-      if (lane < j) {
-        uint64_t *rec = a.lb + (j - 1 - lane) * 8;
-        // all eight words in one round trip
-        const uint64_t a0 = load_agent_u64(rec + 0), a1 = load_agent_u64(rec + 1),
-                       a2 = load_agent_u64(rec + 2), a3 = load_agent_u64(rec + 3),
-                       i0 = load_agent_u64(rec + 4), i1 = load_agent_u64(rec + 5),
-                       i2 = load_agent_u64(rec + 6), i3 = load_agent_u64(rec + 7);
-        const bool inc = (i0 & i1 & i2 & i3) >> 63;
-        v0 = inc ? i0 : a0;
-        v1 = inc ? i1 : a1;
-        v2 = inc ? i2 : a2;
-        v3 = inc ? i3 : a3;
-        st = inc ? 2 : ((a0 & a1 & a2 & a3) >> 62 ? 1 : 0);
-      }
-      const uint64_t zero = bk.ballot(st == 0), incl = bk.ballot(st == 2);
-      const uint32_t fz = zero ? (uint32_t)ctz64(zero) : 64u, fi = incl ? (uint32_t)ctz64(incl) : 64u;
-      const uint32_t take = fi < fz ? fi + 1 : fz;
-      const bool use = lane < take;
-      sh.lbw[4 * lane + 0] = use ? v0 & kValMask : 0;
-      sh.lbw[4 * lane + 1] = use ? v1 & kValMask : 0;
-      sh.lbw[4 * lane + 2] = use ? v2 & kValMask : 0;
-      sh.lbw[4 * lane + 3] = use ? v3 & kValMask : 0;
-      bk.wave_sync();
-      if (lane < 4)
-        for (uint32_t i = 0; i < take; ++i) acc += sh.lbw[4 * i + lane];
-      bk.wave_sync();
-      j -= take;
-      done = fi < fz;
-      if (!done && take == 0) {
-        if (++spins > kSpinLimit) {  // never expected: hand the input to the exact path
-          if (lane == 0) atomic_or_u32(a.gate, 2u);
-          done = true;
-        }
-        spin_pause();
-      }
-    }
+    const uint32_t rounds =
+        look_back(a.lb, k, tid == 0 ? nL : tid == 1 ? nI : tid == 2 ? nV : nW, a.gate, sh.c, bk);
 #if defined(DMLC_AMD_STAMPS) && defined(__HIP_DEVICE_COMPILE__)
-    if (lane == 0 && k < kStampTiles) g_stamps[(uint64_t)k * 8 + 7] = rounds;
+    if (tid == 0 && k < kStampTiles) g_stamps[(uint64_t)k * 8 + 7] = rounds;
 #else
     (void)rounds;
 #endif
-    if (lane < 4) {
-      if (k > 0) {
-        const uint64_t agg = lane == 0 ? nL : lane == 1 ? nI : lane == 2 ? nV : nW;
-        store_agent_u64(a.lb + (uint64_t)k * 8 + 4 + lane, kIncl | (acc + agg));
-      }
-      sh.base[lane] = acc;
-    }
   }
   bk.sync();
-  FSVM_STAMP(k, 5);
-  const uint64_t bRows = sh.base[Q_ROWS], bIdx = sh.base[Q_INDEX], bVal = sh.base[Q_VALUE],
-                 bW = sh.base[Q_WEIGHT];
+  FAST_STAMP(k, 5);
+  const uint64_t bRows = sh.c.base[Q_ROWS], bIdx = sh.c.base[Q_INDEX], bVal = sh.c.base[Q_VALUE],
+                 bW = sh.c.base[Q_WEIGHT];
   // ---- the last tile publishes the totals (dmlc_amd_result.count)
   if (k + 1 == a.ntiles && tid == 0) {
     const uint64_t rows = bRows + nL;
@@ -795,14 +428,14 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk) {
       else raise_error(a.err, E_CAPACITY, q);
     }
   }
-  FSVM_STAMP(k, 6);
+  FAST_STAMP(k, 6);
   // ---- per-chunk exclusive counts at each chunk start in my segment
   if (a.chunk_tab) {
-    for (uint32_t i = 0; i < sh.ncs; ++i) {
-      const uint64_t x = sh.csl[i];
+    for (uint32_t i = 0; i < sh.c.ncs; ++i) {
+      const uint64_t x = sh.c.csl[i];
       if (x < P || x >= P + kSegB || x >= t.thi) continue;
       const uint64_t below = (1ull << (x - P)) - 1;
-      uint64_t *row = a.chunk_tab + (uint64_t)(sh.c_first + i) * 8;
+      uint64_t *row = a.chunk_tab + (uint64_t)(sh.c.c_first + i) * 8;
       const uint64_t rows = eL + popc64(so.L & below);
       row[C_ROWS] = rows;
       row[C_INDEX] = eI + popc64(so.I & below);
