@@ -173,6 +173,13 @@ def main():
     dom_ms = kern_ms / max(launches, 1)
     dom_bytes = nbytes + b_out
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
+    traffic = None
+    try:  # HBM bytes per launch measured by rocprofv3 PMC passes (tools/gpu_pmc.sh) on this kernel
+        tr = json.load(open(os.path.join(ROOT, "profiles", "traffic.json"))).get(args.config)
+        if tr and tr["kernel"] == kern_name and not args.rows and not args.tile_bytes:
+            traffic = tr["hbm_bytes_per_launch"]
+    except (OSError, ValueError):
+        pass
     line = {
         "metric": "device-resident libsvm parse GB/s (input bytes) at 1/2/4/8 GPU; % HBM roofline",
         "value": round(value, 3),
@@ -196,7 +203,7 @@ def main():
         "path": path,
         "roofline": {"bound": "hbm", "kernel": kern_name, "achieved": round(achieved, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "bytes_per_launch": dom_bytes, "avg_ms": round(dom_ms, 4)},
         "cpu_baseline": None,
     }

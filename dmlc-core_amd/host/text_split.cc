@@ -1,0 +1,186 @@
+// text_split.cc -- see text_split.h for the contract and reference citations.
+#include "text_split.h"
+
+#include <dirent.h>
+#include <sys/stat.h>
+
+#include <algorithm>
+#include <cstring>
+
+#include "dmlc/base.h"
+
+namespace dmlc_amd {
+namespace {
+
+bool is_newline(char c) { return c == '\n' || c == '\r'; }
+
+uint64_t file_size(const std::string &p) {
+  struct stat st;
+  if (stat(p.c_str(), &st) != 0) throw dmlc::Error("Check failed: file \"" + p + "\" does not exist");
+  return (uint64_t)st.st_size;
+}
+
+}  // namespace
+
+std::vector<std::string> ListInputFiles(const std::string &path) {
+  std::vector<std::string> out;
+  size_t start = 0;
+  while (start <= path.size()) {
+    size_t end = path.find(';', start);
+    if (end == std::string::npos) end = path.size();
+    std::string p = path.substr(start, end - start);
+    if (p.compare(0, 7, "file://") == 0) p = p.substr(7);
+    if (!p.empty()) {
+      struct stat st;
+      if (stat(p.c_str(), &st) != 0) throw dmlc::Error("Check failed: file \"" + p + "\" does not exist");
+      if (S_ISDIR(st.st_mode)) {
+        std::vector<std::string> ents;
+        if (DIR *d = opendir(p.c_str())) {
+          while (dirent *e = readdir(d)) {
+            std::string q = p + (p.back() == '/' ? "" : "/") + e->d_name;
+            struct stat es;
+            if (e->d_name[0] != '.' && stat(q.c_str(), &es) == 0 && S_ISREG(es.st_mode)) ents.push_back(q);
+          }
+          closedir(d);
+        }
+        std::sort(ents.begin(), ents.end());
+        out.insert(out.end(), ents.begin(), ents.end());
+      } else {
+        out.push_back(p);
+      }
+    }
+    start = end + 1;
+  }
+  return out;
+}
+
+TextSplit::TextSplit(const std::string &uri, unsigned part, unsigned nparts, size_t buffer_bytes)
+    : buffer_bytes_(buffer_bytes) {
+  if (nparts == 0 || part >= nparts) throw dmlc::Error("Check failed: part_index < num_parts");
+  offset_.push_back(0);
+  for (const std::string &f : ListInputFiles(uri)) {
+    const uint64_t sz = file_size(f);
+    if (sz == 0) continue;  // empty files take no part in the split
+    files_.push_back(f);
+    offset_.push_back(offset_.back() + sz);
+  }
+  const uint64_t total = offset_.back();
+  const uint64_t step = (total + nparts - 1) / nparts;
+  offset_begin_ = std::min(step * part, total);
+  offset_end_ = std::min(step * (part + 1), total);
+  if (offset_begin_ < offset_end_) {
+    // move both ends to the next record start, within their files
+    size_t fe = FileOf(offset_end_);
+    if (offset_end_ != offset_[fe]) offset_end_ += SeekRecordBegin(fe, offset_end_ - offset_[fe]);
+    size_t fb = FileOf(offset_begin_);
+    if (offset_begin_ != offset_[fb]) offset_begin_ += SeekRecordBegin(fb, offset_begin_ - offset_[fb]);
+  }
+  BeforeFirst();
+}
+
+TextSplit::~TextSplit() {
+  if (fp_) fclose(fp_);
+}
+
+size_t TextSplit::FileOf(uint64_t off) const {
+  size_t i = 0;
+  while (i + 1 < offset_.size() && offset_[i + 1] <= off) ++i;
+  return std::min(i, files_.empty() ? 0 : files_.size() - 1);
+}
+
+bool TextSplit::OpenAt(size_t file, uint64_t pos) {
+  if (fp_) fclose(fp_);
+  fp_ = nullptr;
+  if (file >= files_.size()) return false;
+  fp_ = fopen(files_[file].c_str(), "rb");
+  if (!fp_) throw dmlc::Error("Check failed: cannot open \"" + files_[file] + "\"");
+  if (fseeko(fp_, (off_t)pos, SEEK_SET) != 0) throw dmlc::Error("Check failed: seek in \"" + files_[file] + "\"");
+  return true;
+}
+
+// Bytes from `pos` in `file` to the next record start: past the first newline
+// run that follows pos (end of file if none).
+uint64_t TextSplit::SeekRecordBegin(size_t file, uint64_t pos) {
+  FILE *f = fopen(files_[file].c_str(), "rb");
+  if (!f) throw dmlc::Error("Check failed: cannot open \"" + files_[file] + "\"");
+  fseeko(f, (off_t)pos, SEEK_SET);
+  uint64_t n = 0;
+  int c;
+  while ((c = fgetc(f)) != EOF) {
+    ++n;
+    if (is_newline((char)c)) break;
+  }
+  if (c != EOF) {
+    while ((c = fgetc(f)) != EOF && is_newline((char)c)) ++n;
+  }
+  fclose(f);
+  return n;
+}
+
+void TextSplit::BeforeFirst() {
+  overflow_.clear();
+  offset_curr_ = offset_begin_;
+  if (offset_begin_ >= offset_end_ || files_.empty()) return;
+  file_ptr_ = FileOf(offset_begin_);
+  OpenAt(file_ptr_, offset_begin_ - offset_[file_ptr_]);
+}
+
+// Up to `size` bytes of the part; a '\n' follows each file's last byte.
+size_t TextSplit::Read(char *buf, size_t size) {
+  if (offset_begin_ >= offset_end_) return 0;
+  if (offset_curr_ + size > offset_end_) size = offset_end_ - offset_curr_;
+  if (size == 0) return 0;
+  size_t left = size;
+  while (fp_) {
+    const size_t n = fread(buf, 1, left, fp_);
+    buf += n;
+    left -= n;
+    offset_curr_ += n;
+    if (left == 0) break;
+    if (n == 0) {  // end of this file: newline, then the next file
+      *buf++ = '\n';
+      --left;
+      if (file_ptr_ + 1 >= files_.size()) break;
+      OpenAt(++file_ptr_, 0);
+    }
+  }
+  return size - left;
+}
+
+bool TextSplit::NextChunk(std::vector<char> *out) {
+  // the reference buffer is buffer_bytes/4 + 1 words with the last one a
+  // sentinel; growing doubles the word count (Chunk::Load), so usable sizes run
+  // B, 2B+4, 4B+12, ...
+  size_t words = buffer_bytes_ / 4 + 1;
+  for (;;) {
+    const size_t cap = (words - 1) * 4;
+    if (cap <= overflow_.size()) {  // a record longer than the buffer: grow it
+      words *= 2;
+      continue;
+    }
+    std::vector<char> buf(cap + 1);
+    std::memcpy(buf.data(), overflow_.data(), overflow_.size());
+    const size_t olen = overflow_.size();
+    size_t n = Read(buf.data() + olen, cap - olen) + olen;
+    if (n == 0) return false;
+    if (n == olen) buf[n++] = '\n';  // end of input mid-record
+    // cut after the last newline (the chunk keeps whole records)
+    size_t cut = 0;
+    for (size_t p = n - 1; p > 0; --p) {
+      if (is_newline(buf[p])) {
+        cut = p + 1;
+        break;
+      }
+    }
+    if (cut == 0) {  // no record boundary yet: keep reading with a bigger buffer
+      overflow_.assign(buf.begin(), buf.begin() + n);
+      words *= 2;
+      continue;
+    }
+    out->insert(out->end(), buf.begin(), buf.begin() + cut);
+    overflow_.assign(buf.begin() + cut, buf.begin() + n);
+    return true;
+  }
+}
+
+}  // namespace dmlc_amd

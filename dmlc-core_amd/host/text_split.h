@@ -1,0 +1,57 @@
+// text_split.h -- host-side text InputSplit with dmlc-core's chunk contract
+// (InputSplit::Create(uri, part, nparts, "text"), src/io.cc:76-119):
+//
+//  * the input is a list of files (a file, a directory's regular files, or a
+//    ';'-separated list), empty files dropped (input_split_base.cc:139-161);
+//  * part k of n covers bytes [ceil(total/n)*k, ceil(total/n)*(k+1)) of the
+//    concatenation, both ends moved forward to the next record start
+//    (ResetPartition, input_split_base.cc:29-63; LineSplitter::SeekRecordBegin,
+//    line_split.cc:11-36);
+//  * chunks fill a read buffer (8 MiB by default, input_split_base.h:39) and are
+//    cut after the last '\n' / '\r' in it (FindLastRecordBegin,
+//    line_split.cc:37-45), the remainder carried into the next chunk; a record
+//    longer than the buffer doubles it (Chunk::Load, input_split_base.cc:272-291);
+//  * a '\n' is inserted after every file's last byte and at the end of input
+//    when the last chunk would otherwise end mid-record (Read / ReadChunk,
+//    input_split_base.cc:204-210, 247-254).
+#pragma once
+#include <cstdint>
+#include <cstdio>
+#include <string>
+#include <vector>
+
+namespace dmlc_amd {
+
+class TextSplit {
+ public:
+  TextSplit(const std::string &uri, unsigned part, unsigned nparts, size_t buffer_bytes = 8u << 20);
+  ~TextSplit();
+  TextSplit(const TextSplit &) = delete;
+  TextSplit &operator=(const TextSplit &) = delete;
+
+  // Appends the next chunk to *out; false at the end of the part.
+  bool NextChunk(std::vector<char> *out);
+  // Rewind to the start of the part.
+  void BeforeFirst();
+  // Bytes of this part's byte range consumed so far.
+  size_t BytesRead() const { return offset_curr_ - offset_begin_; }
+
+ private:
+  size_t Read(char *buf, size_t size);
+  uint64_t SeekRecordBegin(size_t file, uint64_t pos);
+  size_t FileOf(uint64_t off) const;
+  bool OpenAt(size_t file, uint64_t pos);
+
+  std::vector<std::string> files_;
+  std::vector<uint64_t> offset_;  // files_.size() + 1 prefix sums of the sizes
+  uint64_t offset_begin_ = 0, offset_end_ = 0, offset_curr_ = 0;
+  size_t file_ptr_ = 0;
+  FILE *fp_ = nullptr;
+  size_t buffer_bytes_;
+  std::vector<char> overflow_;  // partial record carried to the next chunk
+};
+
+// Expand a URI path (file, directory or ';'-separated list) into file paths.
+std::vector<std::string> ListInputFiles(const std::string &path);
+
+}  // namespace dmlc_amd

@@ -1,0 +1,204 @@
+"""The C++ drop-in layer (include/dmlc/data.h over the C ABI).
+
+CPU: the host InputSplit (dmlc-core_amd/host/text_split.cc) produces the
+reference's chunk sequence (checked against the oracle restatement of
+input_split_base.cc / line_split.cc, itself pinned by tests/golden/split.json).
+GPU: dmlc::Parser / RowBlockIter on real files -- the scenarios of
+test/unittest_inputsplit.cc:41-147 plus synthetic multi-file, multi-part
+inputs -- equal the oracle.
+"""
+import ctypes
+import hashlib
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from golden_util import diff, load_json
+from test_oracle import _regen_files
+from oracle import pyoracle as po
+from tools import synth
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HOST_LIB = os.path.join(ROOT, "dmlc-core_amd", "lib", "libdmlc_amd_host.so")
+DRIVER = os.path.join(ROOT, "tests", "cpp", "_build", "host_api_test")
+
+
+def _host():
+    if not os.path.exists(HOST_LIB):
+        subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "dmlc-core_amd")])
+    L = ctypes.CDLL(HOST_LIB)
+    L.dmlc_amd_host_split.argtypes = [ctypes.c_char_p, ctypes.c_uint, ctypes.c_uint, ctypes.c_uint64,
+                                      ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p),
+                                      ctypes.POINTER(ctypes.c_uint64)]
+    L.dmlc_amd_host_free.argtypes = [ctypes.c_void_p]
+    return L
+
+
+def host_split(uri, part, nparts, buffer_bytes):
+    L = _host()
+    buf, off, n = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_uint64()
+    assert L.dmlc_amd_host_split(uri.encode(), part, nparts, buffer_bytes, ctypes.byref(buf),
+                                 ctypes.byref(off), ctypes.byref(n)) == 0
+    offs = np.ctypeslib.as_array(ctypes.cast(off, ctypes.POINTER(ctypes.c_uint64)), (n.value + 1,)).copy()
+    data = ctypes.string_at(buf, int(offs[-1])) if offs[-1] else b""
+    L.dmlc_amd_host_free(buf)
+    L.dmlc_amd_host_free(off)
+    return [data[int(a):int(b)] for a, b in zip(offs[:-1], offs[1:])]
+
+
+def _write(tmp_path, contents):
+    d = tmp_path / "data"
+    d.mkdir(exist_ok=True)
+    paths = []
+    for i, c in enumerate(contents):
+        p = d / ("part-%02d.txt" % i)
+        p.write_bytes(c)
+        paths.append(str(p))
+    return str(d), paths
+
+
+def _random_files(rng, fmt, nfiles):
+    out = []
+    for i in range(nfiles):
+        t, _ = synth.rows(fmt, int(rng.integers(0, 400)), int(rng.integers(1, 30)), seed=int(rng.integers(1, 99)))
+        b = t.tobytes()
+        if b and rng.random() < 0.4:
+            b = b.rstrip(b"\n")  # a file without a final newline
+        if rng.random() < 0.2:
+            b = b.replace(b"\n", b"\r\n")
+        out.append(b)
+    return out
+
+
+def test_host_split_matches_oracle(tmp_path):
+    rng = np.random.default_rng(2)
+    for it in range(12):
+        contents = _random_files(rng, synth.LIBSVM, int(rng.integers(1, 5)))
+        d, paths = _write(tmp_path, contents)
+        uri = ";".join(paths) if it % 2 else d
+        nparts = int(rng.integers(1, 5))
+        buf = int(rng.choice([64, 1000, 1 << 16, 8 << 20]))
+        for part in range(nparts):
+            got = host_split(uri, part, nparts, buf)
+            exp = po.split_text(contents, part, nparts, buffer_bytes=buf)
+            assert got == exp, (it, part, nparts, buf)
+        for p in paths:
+            os.remove(p)
+
+
+@pytest.mark.parametrize("case", load_json("split.json")["cases"],
+                         ids=lambda c: "%s-%d/%d" % (c["name"], c["part"], c["nparts"]))
+def test_host_split_golden_chunking(case, tmp_path):
+    """The InputSplit chunkings recorded from the genuine reference (tests/golden/split.json)."""
+    files = _regen_files(case)
+    paths = []
+    for i, fn in enumerate(case["order"]):  # the reference's file order
+        p = tmp_path / ("%02d_%s" % (i, fn))
+        p.write_bytes(files[fn])
+        paths.append(str(p))
+    got = host_split(";".join(paths), case["part"], case["nparts"], 8 << 20)
+    assert [len(c) for c in got] == case["chunk_sizes"]
+    assert [hashlib.sha256(c).hexdigest() for c in got] == case["chunk_sha256"]
+
+
+# ------------------------------------------------------------------ GPU --
+
+def _driver():
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "tests", "cpp")])
+    return DRIVER
+
+
+def run_api(tmp_path, uri, part=0, nparts=1, fmt="libsvm", index_bits=32, dtype="f32", iter_=False):
+    o = str(tmp_path / "out")
+    args = [_driver(), uri, str(part), str(nparts), fmt, str(index_bits), dtype, o] + (["iter"] if iter_ else [])
+    r = subprocess.run(args, capture_output=True)
+    if r.returncode == 3:
+        return {"error": open(o + ".error").read()}
+    assert r.returncode == 0, r.stderr.decode()[-2000:]
+    it = np.uint64 if index_bits == 64 else np.uint32
+    vt = {"f32": np.float32, "i32": np.int32, "i64": np.int64}[dtype]
+    h = {"offset": np.fromfile(o + ".offset", np.uint64), "label": np.fromfile(o + ".label", vt),
+         "weight": np.fromfile(o + ".weight", np.float32), "qid": np.fromfile(o + ".qid", np.uint64),
+         "index": np.fromfile(o + ".index", it), "value": np.fromfile(o + ".value", vt),
+         "meta": np.fromfile(o + ".meta", np.uint64)}
+    return h
+
+
+def oracle_files(contents, part=0, nparts=1, fmt=po.LIBSVM, **kw):
+    chunks = po.split_text(contents, part, nparts)
+    offs = np.cumsum([0] + [len(c) for c in chunks]).tolist()
+    return po.parse_chunks(b"".join(chunks), offs, fmt=fmt, **kw), len(chunks)
+
+
+@pytest.mark.gpu
+def test_api_unittest_inputsplit_scenarios(tmp_path):
+    """test/unittest_inputsplit.cc:41-147 through dmlc::Parser::Create."""
+    # CSV across three files, one without a final newline (:41-68)
+    csv = [b"0,1,2,3\n4,5,6,7\n", b"8,9,10,11\n12,13,14,15", b"16,17,18,19\n"]
+    d, _ = _write(tmp_path / "csv", csv)
+    h = run_api(tmp_path, d, fmt="csv")
+    o, _ = oracle_files(csv, fmt=po.CSV)
+    assert "error" not in h and diff(h, o) == [] and len(h["offset"]) - 1 == 5
+    # libsvm, no final newline (:70-92)
+    svm = [b"1 1:1 2:2\n0 3:3\n1 4:4 5:5"]
+    d, _ = _write(tmp_path / "svm", svm)
+    h = run_api(tmp_path, d)
+    o, _ = oracle_files(svm)
+    assert diff(h, o) == [] and len(h["offset"]) - 1 == 3
+    # five files (:94-116) and two parts of ten lines -> {6, 4} rows (:118-147)
+    lines = [b"%d %d:1\n" % (i % 2, i) for i in range(10)]
+    five = [b"".join(lines[2 * i:2 * i + 2]) for i in range(5)]
+    d, _ = _write(tmp_path / "five", five)
+    h = run_api(tmp_path, d)
+    assert len(h["offset"]) - 1 == 10
+    rows = []
+    for part in range(2):
+        h = run_api(tmp_path, d, part, 2)
+        o, _ = oracle_files(five, part, 2)
+        assert diff(h, o) == []
+        rows.append(len(h["offset"]) - 1)
+    assert rows == [6, 4]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fmt", ["libsvm", "csv"])
+def test_api_synthetic_multifile_multipart(tmp_path, fmt):
+    rng = np.random.default_rng(11 if fmt == "libsvm" else 12)
+    f = synth.LIBSVM if fmt == "libsvm" else synth.CSV
+    contents = _random_files(rng, f, 4)
+    d, _ = _write(tmp_path / fmt, contents)
+    for nparts in (1, 3):
+        for part in range(nparts):
+            h = run_api(tmp_path, d, part, nparts, fmt)
+            o, nch = oracle_files(contents, part, nparts, fmt=po.LIBSVM if fmt == "libsvm" else po.CSV)
+            assert diff(h, o) == [], (part, nparts)
+
+
+@pytest.mark.gpu
+def test_api_large_multibatch_and_rowiter(tmp_path, monkeypatch):
+    """Several 8 MiB chunks and several device batches; RowBlockIter concat + NumCol."""
+    text, _ = synth.rows(synth.LIBSVM, 60000, 128, seed=4)
+    d, _ = _write(tmp_path / "big", [text.tobytes()])
+    monkeypatch.setenv("DMLC_AMD_BATCH_BYTES", str(24 << 20))
+    h = run_api(tmp_path, d)
+    o, nch = oracle_files([text.tobytes()])
+    assert diff(h, o) == []
+    assert int(h["meta"][0]) == nch and int(h["meta"][1]) == len(text)
+    hi = run_api(tmp_path, d, iter_=True)
+    assert diff(hi, o) == [] and int(hi["meta"][2]) == int(o["index"].max()) + 1
+
+
+@pytest.mark.gpu
+def test_api_errors_and_args(tmp_path):
+    d, _ = _write(tmp_path / "neg", [b"1 -3:1\n"])
+    assert "sign == true" in run_api(tmp_path, d)["error"]
+    d2, _ = _write(tmp_path / "ok", [b"1 3:1\n"])
+    assert "Cannot find argument" in run_api(tmp_path, d2 + "?bogus=1")["error"]
+    h = run_api(tmp_path, d2 + "?indexing_mode=1")
+    assert h["index"].tolist() == [2]
+    d3, _ = _write(tmp_path / "lab", [b"1,2,3\n4,5,6\n"])
+    h = run_api(tmp_path, d3 + "?format=csv&label_column=0", fmt="auto")
+    o, _ = oracle_files([b"1,2,3\n4,5,6\n"], fmt=po.CSV, label_column=0)
+    assert diff(h, o) == []
