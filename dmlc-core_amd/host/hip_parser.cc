@@ -320,11 +320,11 @@ class HipParser : public dmlc::Parser<IndexType, DType> {
                          reinterpret_cast<dmlc_amd_result *>(d_res), stream_));
     // results into pinned host arrays
     h_off_.reserve(c[DMLC_AMD_ROWS] + 1);
-    h_label_.reserve(c[DMLC_AMD_LABEL] + 1);
+    h_label_.reserve((c[DMLC_AMD_LABEL] + 1) * vsz);  // byte arrays
     h_weight_.reserve(c[DMLC_AMD_WEIGHT] + 1);
     h_qid_.reserve(c[DMLC_AMD_QID] + 1);
-    h_index_.reserve(c[DMLC_AMD_INDEX] + 1);
-    h_value_.reserve(c[DMLC_AMD_VALUE] + 1);
+    h_index_.reserve((c[DMLC_AMD_INDEX] + 1) * isz);
+    h_value_.reserve((c[DMLC_AMD_VALUE] + 1) * vsz);
     h_tab_.reserve((size_t)nchunks * 8);
     auto d2h = [&](void *dst, const void *src, size_t bytes) {
       if (bytes) hip_check(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, stream_), "D2H");

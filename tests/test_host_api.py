@@ -50,7 +50,7 @@ def host_split(uri, part, nparts, buffer_bytes):
 
 def _write(tmp_path, contents):
     d = tmp_path / "data"
-    d.mkdir(exist_ok=True)
+    d.mkdir(parents=True, exist_ok=True)
     paths = []
     for i, c in enumerate(contents):
         p = d / ("part-%02d.txt" % i)
@@ -122,7 +122,7 @@ def run_api(tmp_path, uri, part=0, nparts=1, fmt="libsvm", index_bits=32, dtype=
     h = {"offset": np.fromfile(o + ".offset", np.uint64), "label": np.fromfile(o + ".label", vt),
          "weight": np.fromfile(o + ".weight", np.float32), "qid": np.fromfile(o + ".qid", np.uint64),
          "index": np.fromfile(o + ".index", it), "value": np.fromfile(o + ".value", vt),
-         "meta": np.fromfile(o + ".meta", np.uint64)}
+         "field": np.zeros(0, it), "meta": np.fromfile(o + ".meta", np.uint64)}
     return h
 
 
@@ -173,6 +173,7 @@ def test_api_synthetic_multifile_multipart(tmp_path, fmt):
         for part in range(nparts):
             h = run_api(tmp_path, d, part, nparts, fmt)
             o, nch = oracle_files(contents, part, nparts, fmt=po.LIBSVM if fmt == "libsvm" else po.CSV)
+            assert "error" not in h, (h, part, nparts, [len(c) for c in contents])
             assert diff(h, o) == [], (part, nparts)
 
 
