@@ -20,6 +20,13 @@ struct DevBlock {
     __builtin_amdgcn_wave_barrier();
   }
 
+  // sum over the 64 lanes of the calling wave (all lanes active)
+  __device__ __forceinline__ uint32_t wave_sum(uint32_t v) const {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, kWave);
+    return v;
+  }
+
   template <typename T>
   __device__ __forceinline__ static T shfl_up(T v, int d) {
     static_assert(sizeof(T) % 4 == 0, "4-byte granular");

@@ -131,6 +131,70 @@ DA_HD Masks classify64(const uint8_t *p) {
   return m;
 }
 
+// ---- byte classes by table lookup (the VALU-cheap form on MI355X: one SDWA
+// shift + one shift-or per byte, the lookup on the LDS pipe).  Entry planes:
+// byte 0 D digitchar, 1 G digit, 2 N newline, 3 C colon; blanks are 0; a byte
+// outside the grammar is G without D.
+DA_HD uint32_t class_of(uint32_t b) {
+  if (b - '0' < 10u) return 0x00000101u;
+  if (b == '+' || b == '-' || b == '.' || b == 'e' || b == 'E') return 0x00000001u;
+  if (b == '\n' || b == '\r') return 0x00010000u;
+  if (b == ':') return 0x01000000u;
+  if (b == ' ' || b == '\t') return 0u;
+  return 0x00000100u;
+}
+
+// Masks of the 64 bytes at p (16-byte aligned) through the class table.
+DA_HD Masks classify64_lut(const uint8_t *p, const uint32_t *cls) {
+  uint32_t acc[8];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    uint32_t w[4];
+    load16(p + 16 * q, w);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const int i = 16 * q + 4 * j + b;
+        const uint32_t x = cls[(w[j] >> (8 * b)) & 0xFFu];
+        if ((i & 7) == 0) acc[i >> 3] = x;
+        else acc[i >> 3] |= x << (i & 7);
+      }
+  }
+  // byte p of acc[j] = plane p of bytes 8j..8j+7: gather plane bytes
+  uint32_t pd[2], pg[2], pn[2], pc[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const uint32_t t = perm_b32(acc[4 * h + 1], acc[4 * h], 0x05010400u);
+    const uint32_t u = perm_b32(acc[4 * h + 3], acc[4 * h + 2], 0x05010400u);
+    pd[h] = perm_b32(u, t, 0x05040100u);
+    pg[h] = perm_b32(u, t, 0x07060302u);
+    const uint32_t t2 = perm_b32(acc[4 * h + 1], acc[4 * h], 0x07030602u);
+    const uint32_t u2 = perm_b32(acc[4 * h + 3], acc[4 * h + 2], 0x07030602u);
+    pn[h] = perm_b32(u2, t2, 0x05040100u);
+    pc[h] = perm_b32(u2, t2, 0x07060302u);
+  }
+  Masks m;
+  m.d = pd[0] | ((uint64_t)pd[1] << 32);
+  m.n = pn[0] | ((uint64_t)pn[1] << 32);
+  m.c = pc[0] | ((uint64_t)pc[1] << 32);
+  const uint64_t g = pg[0] | ((uint64_t)pg[1] << 32);
+  m.bad = (g & ~m.d) != 0;
+  return m;
+}
+// 4 bytes (x) through the table: 4-bit masks
+DA_HD Nib classify_dword_lut(uint32_t x, const uint32_t *cls) {
+  uint32_t acc = 0;
+#pragma unroll
+  for (int b = 0; b < 4; ++b) acc |= cls[(x >> (8 * b)) & 0xFFu] << b;
+  Nib r;
+  r.d = acc & 0xFu;
+  r.n = (acc >> 16) & 0xFu;
+  r.c = (acc >> 24) & 0xFu;
+  r.bad = ((acc >> 8) & ~acc & 0xFu) != 0;
+  return r;
+}
+
 struct AddU64 {
   DA_HD uint64_t operator()(uint64_t a, uint64_t b) const { return a + b; }
 };
@@ -272,6 +336,119 @@ DA_HD bool wuint(const W16 &w, bool wide, uint64_t *out, bool *ok) {
   return true;
 }
 
+// ---- 32-bit decoders (MI355X: v_dot4_u32_u8, 32-bit mul and perm are full
+// rate; 64-bit multiplies and the f64 divide sequence are not)
+struct DecTables {
+  double p10[16], i10[16];  // 10^k and RN(10^-k)
+  uint32_t inv5[9];         // 5^-k mod 2^32
+};
+template <class BK>
+DA_HDF void init_dec_tables(DecTables &tb, BK &bk) {
+  const int t = bk.tid();
+  if (t < 16) {
+    double p = 1.0;
+    for (int i = 0; i < t; ++i) p *= 10.0;
+    tb.p10[t] = p;
+    tb.i10[t] = 1.0 / p;  // correctly rounded reciprocal (IEEE division)
+  } else if (t < 25) {
+    uint32_t v = 1;
+    for (int i = 0; i < t - 16; ++i) v *= 0xCCCCCCCDu;  // 5^-1 mod 2^32
+    tb.inv5[t - 16] = v;
+  }
+}
+DA_HD uint32_t udot4(uint32_t a, uint32_t b, uint32_t c) {  // sum of the 4 byte products + c
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_udot4(a, b, c, false);
+#else
+  for (int i = 0; i < 4; ++i) c += ((a >> (8 * i)) & 0xFFu) * ((b >> (8 * i)) & 0xFFu);
+  return c;
+#endif
+}
+// acc * 10^4 + the 4-digit value of the nibbles d (byte 0 most significant)
+DA_HD uint32_t dig4(uint32_t d, uint32_t acc) {
+  const uint32_t t = udot4(d, 0x0000010Au, acc * 100u);  // acc*100 + 10 d0 + d1
+  return udot4(d, 0x010A0000u, t * 100u);                // t*100 + 10 d2 + d3
+}
+DA_HD uint32_t nd4(uint32_t x) {  // 4 bits: byte i is not '0'..'9' (bytes < 0x80)
+  return udot4((((x ^ 0x30303030u) + 0x76767676u) >> 7) & 0x01010101u, 0x08040201u, 0u);
+}
+DA_HD uint32_t byte_of(const uint32_t w[4], uint32_t p) {  // window byte p < 16
+  const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3];
+  const uint32_t a = (p & 4u) ? w1 : w0, b = (p & 4u) ? w3 : w2;
+  return ((p & 8u ? b : a) >> (8u * (p & 3u))) & 0xFFu;
+}
+DA_HD uint64_t low_bytes(uint32_t k) {  // mask of the low k bytes, k <= 8
+  return k >= 8 ? ~0ull : ((1ull << (8u * k)) - 1ull);
+}
+// the 8 window bytes from byte s (s <= 1) as nibbles, keeping the first L
+DA_HD uint32_t lead8(const uint32_t w[4], uint32_t s, uint32_t L) {
+  const uint32_t lo = funnel(w[1], w[0], 8u * s), hi = funnel(w[2], w[1], 8u * s);
+  const uint64_t m = low_bytes(L) & 0x0F0F0F0F0F0F0F0Full;
+  return dig4(hi & (uint32_t)(m >> 32), dig4(lo & (uint32_t)m, 0u));  // = value * 10^(8-L)
+}
+
+// ParseFloat<float> (strtonum.h:95-264) on a run of the uniform grammar,
+// 32-bit form: integer part (<= 8 digits) left-aligned in 8 nibbles then an
+// exact division by 10^(8-il) (shift + multiply by 5^-k mod 2^32); fraction
+// digits kept in place in the 16-byte window, V = val2 * 10^(16-pe) < 10^15,
+// so V / 10^(16-fs) is the same real number as val2 / 10^fl and its
+// correctly rounded double is the reference's (double)val2/(double)pow10,
+// computed as a Markstein quotient (one multiply, two FMAs, tabulated
+// reciprocal).  *ok = false: exponent, long parts or a number that may
+// continue past the window (caller falls back to the byte decoder).
+DA_HD float wfloat32(const uint32_t w[4], const DecTables &tb, bool *ok) {
+  const uint32_t M = nd4(w[0]) | (nd4(w[1]) << 4) | (nd4(w[2]) << 8) | (nd4(w[3]) << 12);
+  const uint32_t b0 = w[0] & 0xFFu;
+  const bool neg = b0 == '-';
+  const uint32_t sg = (neg || b0 == '+') ? 1u : 0u;
+  const uint32_t p = (uint32_t)ctz32((M & ~sg) | 0x10000u);
+  *ok = false;
+  if (p >= 16u) return 0.f;
+  const uint32_t c = byte_of(w, p);
+  const bool dot = c == '.';
+  const uint32_t fs = p + 1u;
+  const uint32_t pe = dot ? (uint32_t)ctz32((M & ~((2u << p) - 1u)) | 0x10000u) : p;
+  if (pe >= 16u) return 0.f;
+  const uint32_t ce = dot ? byte_of(w, pe) : c;
+  const uint32_t il = p - sg;
+  if ((ce | 0x20u) == 'e' || il > 8u) return 0.f;
+  const uint32_t iv8 = lead8(w, sg, il);
+  const uint32_t k = 8u - il;
+  const uint32_t iv = (iv8 >> k) * tb.inv5[k];
+  // fraction bytes [fs, pe) (empty without a '.')
+  const uint64_t mlo = (low_bytes(pe) & ~low_bytes(fs)) & 0x0F0F0F0F0F0F0F0Full;
+  const uint64_t mhi = (low_bytes(pe > 8u ? pe - 8u : 0u) & ~low_bytes(fs > 8u ? fs - 8u : 0u)) &
+                       0x0F0F0F0F0F0F0F0Full;
+  const uint32_t fh = dig4(w[1] & (uint32_t)(mlo >> 32), dig4(w[0] & (uint32_t)mlo, 0u));
+  const uint32_t fo = dig4(w[3] & (uint32_t)(mhi >> 32), dig4(w[2] & (uint32_t)mhi, 0u));
+  const double v = __builtin_fma((double)fh, 1e8, (double)fo);  // exact: < 10^15
+  const uint32_t e = 16u - fs;                                  // 1..15
+  const double r = tb.i10[e], t = v * r;
+  const double q = __builtin_fma(r, __builtin_fma(-t, tb.p10[e], v), t);
+  const float value = (float)iv + (float)q;
+  *ok = true;
+  return neg ? -value : value;
+}
+
+// ParseUnsignedInt (strtonum.h:392-428): [+] then up to 8 digits.  Returns
+// false on a leading '-' (the reference's fatal CHECK); *ok = false when the
+// digits may not fit the form (caller falls back).
+DA_HD bool wuint32(const uint32_t w[4], const DecTables &tb, uint64_t *out, bool *ok) {
+  const uint32_t b0 = w[0] & 0xFFu;
+  *ok = true;
+  if (b0 == '-') return false;
+  const uint32_t s = b0 == '+' ? 1u : 0u;
+  const uint32_t M = nd4(w[0]) | (nd4(w[1]) << 4) | (nd4(w[2]) << 8) | 0x1000u;
+  const uint32_t L = (uint32_t)ctz32(M & ~s) - s;
+  if (L > 8u) {
+    *ok = false;
+    return true;
+  }
+  const uint32_t k = 8u - L;
+  *out = (lead8(w, s, L) >> k) * tb.inv5[k];
+  return true;
+}
+
 // the 16 bytes at absolute position q (staged in LDS at `text`, which holds
 // position tlo - kPre at index 0; q < tile end) as a window
 DA_HD W16 win_at(const uint8_t *text, uint64_t tlo, uint64_t q) {
@@ -343,70 +520,96 @@ DA_HDF void stage(const uint8_t *text, uint64_t n, uint64_t tlo, TileCommon &c, 
   }
 }
 
-// Lanes 0..3: publish this tile's aggregate (record words 0-3; the inclusive
-// prefix later goes to words 4-7, so a reader never mixes the two).
-DA_HD void publish_aggregate(uint64_t *lb, uint32_t k, int lane, uint64_t agg) {
-  uint64_t *rec = lb + (uint64_t)k * 8;
-  if (k == 0) store_agent_u64(rec + 4 + lane, kIncl | agg);
-  else store_agent_u64(rec + lane, kAgg | agg);
+// ---- decoupled look-back records: 8 words (one 64-byte line) per tile.
+// Word 0 = status (bits 62-63: 1 aggregate, 2 inclusive) | the tile's four
+// counts packed 15 bits each (a 16 KiB tile holds < 2^15 of anything);
+// words 1..4 = the inclusive prefix per counter, written and drained
+// (vmcnt(0)) before the status turns inclusive.  A reader polls ONE word per
+// predecessor and loads the inclusive words only from the one lane that
+// needs them -- polls are the bulk of this kernel's memory requests.
+constexpr uint64_t kSAgg = 1ull << 62, kSIncl = 2ull << 62;
+DA_HD uint64_t pack4(const uint32_t c[4]) {
+  return (uint64_t)c[0] | ((uint64_t)c[1] << 15) | ((uint64_t)c[2] << 30) | ((uint64_t)c[3] << 45);
+}
+DA_HD void drain_stores() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
 }
 
-// Wave 0: decoupled look-back.  Lane i reads predecessor j-1-i's record; a
-// round consumes predecessors up to the first inclusive one and stops before
-// the first unpublished one.  Lanes 0..3 end with c.base[lane] = exclusive
-// prefix of counter `lane` and publish the inclusive prefix (agg = this
-// tile's count).  Returns the number of rounds.  The caller synchronises.
+// Lane 0: publish this tile's aggregate (tile 0 publishes its inclusive).
+DA_HD void publish_aggregate(uint64_t *lb, uint32_t k, const uint32_t cnt[4]) {
+  uint64_t *rec = lb + (uint64_t)k * 8;
+  if (k == 0) {
+    for (int i = 0; i < 4; ++i) store_agent_u64(rec + 1 + i, cnt[i]);
+    drain_stores();
+    store_agent_u64(rec, kSIncl | pack4(cnt));
+  } else {
+    store_agent_u64(rec, kSAgg | pack4(cnt));
+  }
+}
+
+// Wave 0: decoupled look-back.  Lane i polls predecessor j-1-i's status word;
+// a round consumes predecessors up to the first inclusive one and stops
+// before the first unpublished one.  cnt = this tile's counts (wave
+// uniform).  Ends with c.base[0..3] = exclusive prefixes, and publishes the
+// inclusive prefix.  Returns the number of rounds.  The caller synchronises.
 template <class BK>
-DA_HDF uint32_t look_back(uint64_t *lb, uint32_t k, uint64_t agg, uint32_t *gate, TileCommon &c,
+DA_HDF uint32_t look_back(uint64_t *lb, uint32_t k, const uint32_t cnt[4], uint32_t *gate, TileCommon &c,
                           BK &bk) {
   const uint32_t lane = bk.tid();
   uint64_t j = k;
   uint32_t spins = 0, rounds = 0;
-  uint64_t acc = 0;  // lane c < 4: counter c
+  uint64_t acc[4] = {0, 0, 0, 0};
   bool done = k == 0;
   while (!done) {
     ++rounds;
-    uint64_t v0 = 0, v1 = 0, v2 = 0, v3 = 0;
+    uint64_t s = 0;
     uint32_t st = 2;  // before tile 0: an inclusive 0
     if (lane < j) {
-      uint64_t *rec = lb + (j - 1 - lane) * 8;
-      // all eight words in one round trip
-      const uint64_t a0 = load_agent_u64(rec + 0), a1 = load_agent_u64(rec + 1),
-                     a2 = load_agent_u64(rec + 2), a3 = load_agent_u64(rec + 3),
-                     i0 = load_agent_u64(rec + 4), i1 = load_agent_u64(rec + 5),
-                     i2 = load_agent_u64(rec + 6), i3 = load_agent_u64(rec + 7);
-      const bool inc = (i0 & i1 & i2 & i3) >> 63;
-      v0 = inc ? i0 : a0;
-      v1 = inc ? i1 : a1;
-      v2 = inc ? i2 : a2;
-      v3 = inc ? i3 : a3;
-      st = inc ? 2 : ((a0 & a1 & a2 & a3) >> 62 ? 1 : 0);
+      s = load_agent_u64(lb + (j - 1 - lane) * 8);
+      st = (uint32_t)(s >> 62);
     }
     const uint64_t zero = bk.ballot(st == 0), incl = bk.ballot(st == 2);
     const uint32_t fz = zero ? (uint32_t)ctz64(zero) : 64u, fi = incl ? (uint32_t)ctz64(incl) : 64u;
-    const uint32_t take = fi < fz ? fi + 1 : fz;
-    const bool use = lane < take;
-    c.lbw[4 * lane + 0] = use ? v0 & kValMask : 0;
-    c.lbw[4 * lane + 1] = use ? v1 & kValMask : 0;
-    c.lbw[4 * lane + 2] = use ? v2 & kValMask : 0;
-    c.lbw[4 * lane + 3] = use ? v3 & kValMask : 0;
-    bk.wave_sync();
-    if (lane < 4)
-      for (uint32_t i = 0; i < take; ++i) acc += c.lbw[4 * i + lane];
-    bk.wave_sync();
-    j -= take;
+    const uint32_t tagg = fi < fz ? fi : fz;  // lanes below contribute their aggregates
+    const uint64_t mine = lane < tagg ? s : 0ull;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i] += bk.wave_sum((uint32_t)((mine >> (15 * i)) & 0x7FFFu));
     done = fi < fz;
-    if (!done && take == 0) {
-      if (++spins > kSpinLimit) {  // never expected: hand the input to the exact path
-        if (lane == 0) atomic_or_u32(gate, 2u);
-        done = true;
+    if (done) {
+      if ((uint64_t)fi < j) {  // a real inclusive record (else: the start, 0)
+        if (lane == fi) {
+          const uint64_t *rec = lb + (j - 1 - fi) * 8;
+          for (int i = 0; i < 4; ++i) c.lbw[i] = load_agent_u64(const_cast<uint64_t *>(rec) + 1 + i);
+        }
+        bk.wave_sync();
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i] += c.lbw[i];
+        bk.wave_sync();
       }
-      spin_pause();
+    } else {
+      j -= tagg;
+      if (tagg == 0) {
+        if (++spins > kSpinLimit) {  // never expected: hand the input to the exact path
+          if (lane == 0) atomic_or_u32(gate, 2u);
+          done = true;
+        }
+        spin_pause();
+      }
     }
   }
-  if (lane < 4) {
-    if (k > 0) store_agent_u64(lb + (uint64_t)k * 8 + 4 + lane, kIncl | (acc + agg));
-    c.base[lane] = acc;
+  if (lane < 4) c.base[lane] = acc[lane == 0 ? 0 : lane == 1 ? 1 : lane == 2 ? 2 : 3];
+  if (k > 0) {
+    uint64_t *rec = lb + (uint64_t)k * 8;
+    if (lane < 4) {
+      const uint64_t v = acc[lane == 0 ? 0 : lane == 1 ? 1 : lane == 2 ? 2 : 3];
+      const uint32_t cv = cnt[lane == 0 ? 0 : lane == 1 ? 1 : lane == 2 ? 2 : 3];
+      store_agent_u64(rec + 1 + lane, v + cv);
+    }
+    drain_stores();
+    bk.wave_sync();
+    if (lane == 0) store_agent_u64(rec, kSIncl | pack4(cnt));
   }
   return rounds;
 }

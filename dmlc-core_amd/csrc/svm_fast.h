@@ -36,6 +36,8 @@ enum { Q_ROWS = 0, Q_INDEX = 1, Q_VALUE = 2, Q_WEIGHT = 3 };
 
 struct Shared {  // LDS of one workgroup
   TileCommon c;
+  uint32_t cls[256];  // byte class table (fast_common.h class_of)
+  DecTables dt;
   uint64_t md[kThreads + 1];  // slot 0: the segment before the tile; slot t+1: segment t
   uint64_t mn[kThreads + 1];
   uint64_t mc[kThreads + 1];
@@ -242,6 +244,8 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk) {
     chunk_list(a.cs, a.nchunk, t.tlo, t.thi, sh.c);
     sh.md[0] = sh.mn[0] = sh.mc[0] = 0;
   }
+  sh.cls[tid] = class_of((uint32_t)tid);
+  init_dec_tables(sh.dt, bk);
   stage(a.text, a.n, t.tlo, sh.c, bk);
   bk.sync();
   FAST_STAMP(k, 2);
@@ -249,7 +253,7 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk) {
   // of the 64 bytes before the tile -> slot 0
   uint32_t bad = 0;
   {
-    const Masks m = classify64(sh.c.text + kPre + tid * kSegB);
+    const Masks m = classify64_lut(sh.c.text + kPre + tid * kSegB, sh.cls);
     sh.md[tid + 1] = m.d;
     sh.mn[tid + 1] = m.n;
     sh.mc[tid + 1] = m.c;
@@ -257,7 +261,7 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk) {
     if (tid < 16 && t.tlo > 0) {
       uint32_t x;
       memcpy(&x, sh.c.text + 4 * tid, 4);
-      const Nib b = classify_dword(x);
+      const Nib b = classify_dword_lut(x, sh.cls);
       atomic_or_u64(&sh.md[0], (uint64_t)b.d << (4 * tid));
       atomic_or_u64(&sh.mn[0], (uint64_t)b.n << (4 * tid));
       atomic_or_u64(&sh.mc[0], (uint64_t)b.c << (4 * tid));
@@ -278,9 +282,10 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk) {
   const uint32_t nL = (uint32_t)(totp & 0xFFFF), nW = (uint32_t)((totp >> 16) & 0xFFFF),
                  nI = (uint32_t)((totp >> 32) & 0xFFFF), nV = (uint32_t)(totp >> 48);
   // ---- publish this tile's aggregate
-  if (tid < 4) {
-    publish_aggregate(a.lb, k, tid, tid == 0 ? nL : tid == 1 ? nI : tid == 2 ? nV : nW);
-    if (tid == 0 && sh.c.bad) atomic_or_u32(a.gate, 1u);
+  const uint32_t cnt4[4] = {nL, nI, nV, nW};  // look-back slots Q_ROWS, Q_INDEX, Q_VALUE, Q_WEIGHT
+  if (tid == 0) {
+    publish_aggregate(a.lb, k, cnt4);
+    if (sh.c.bad) atomic_or_u32(a.gate, 1u);
   }
   // ---- first decode batch into registers (gives predecessors time to publish)
   const uint64_t P = t.tlo + (uint64_t)tid * kSegB;
@@ -296,7 +301,11 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk) {
     const uint64_t lim = lim_of(q);
     bool ok = false;
     float v = 0.f;
-    if (q + 16 <= lim) v = wfloat(win_at(sh.c.text, t.tlo, q), &ok);
+    if (q + 16 <= lim) {
+      const W16 wq = win_at(sh.c.text, t.tlo, q);
+      const uint32_t w4[4] = {(uint32_t)wq.lo, (uint32_t)(wq.lo >> 32), (uint32_t)wq.hi, (uint32_t)(wq.hi >> 32)};
+      v = wfloat32(w4, sh.dt, &ok);
+    }
     if (!ok) {
       src.lim = lim;
       uint64_t e;
@@ -309,7 +318,11 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk) {
     const uint64_t lim = lim_of(q);
     uint64_t v = 0;
     bool ok = false, pos = true;
-    if (q + 16 <= lim) pos = wuint(win_at(sh.c.text, t.tlo, q), a.wide != 0, &v, &ok);
+    if (q + 16 <= lim) {
+      const W16 wq = win_at(sh.c.text, t.tlo, q);
+      const uint32_t w4[4] = {(uint32_t)wq.lo, (uint32_t)(wq.lo >> 32), (uint32_t)wq.hi, (uint32_t)(wq.hi >> 32)};
+      pos = wuint32(w4, sh.dt, &v, &ok);
+    }
     if (!ok) {
       src.lim = lim;
       pos = parse_uint(src, q, a.wide != 0, &v);
@@ -346,7 +359,7 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk) {
   // ---- decoupled look-back by wave 0 (fast_common.h)
   if (tid < kWave) {
     const uint32_t rounds =
-        look_back(a.lb, k, tid == 0 ? nL : tid == 1 ? nI : tid == 2 ? nV : nW, a.gate, sh.c, bk);
+        look_back(a.lb, k, cnt4, a.gate, sh.c, bk);
 #if defined(DMLC_AMD_STAMPS) && defined(__HIP_DEVICE_COMPILE__)
     if (tid == 0 && k < kStampTiles) g_stamps[(uint64_t)k * 8 + 7] = rounds;
 #else

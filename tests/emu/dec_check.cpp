@@ -1,0 +1,88 @@
+// TEST INFRASTRUCTURE ONLY: the 32-bit window decoders of fast_common.h
+// (wfloat32 / wuint32) against the exact byte decoders of decode.h on
+// generated number strings; every string the window form accepts must decode
+// bit-identically.  usage: dec_check <count> <seed>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+
+#include "fast_common.h"
+
+using namespace dmlc_amd;
+using namespace dmlc_amd::fast;
+
+struct Blk {
+  int t;
+  int tid() const { return t; }
+};
+
+static uint64_t st = 88172645463325252ull;
+static uint64_t rnd() {
+  st ^= st << 13;
+  st ^= st >> 7;
+  st ^= st << 17;
+  return st;
+}
+
+static std::string gen() {
+  std::string s;
+  const int kind = (int)(rnd() % 10);
+  if (rnd() % 8 == 0) s += "+-"[rnd() % 2];
+  if (kind < 6) {  // %.9g-like canonical values
+    char buf[64];
+    const double x = (double)(rnd() % 16777216) / 16777216.0 * (rnd() % 4 == 0 ? 100.0 : 1.0);
+    snprintf(buf, sizeof buf, "%.*g", (int)(1 + rnd() % 12), x);
+    s += buf;
+  } else {  // random digitchar soup
+    const char *al = "0123456789012345678901234567890123456789..eE+-";
+    const int n = 1 + (int)(rnd() % 18);
+    for (int i = 0; i < n; ++i) s += al[rnd() % strlen(al)];
+  }
+  return s;
+}
+
+int main(int argc, char **argv) {
+  const long n = argc > 1 ? atol(argv[1]) : 1000000;
+  st ^= argc > 2 ? (uint64_t)atoll(argv[2]) * 0x9E3779B97F4A7C15ull : 0;
+  DecTables tb;
+  for (int t = 0; t < 32; ++t) {
+    Blk b{t};
+    init_dec_tables(tb, b);
+  }
+  long fast_f = 0, fast_i = 0, bad = 0;
+  for (long it = 0; it < n; ++it) {
+    std::string s = gen();
+    s += " :\n"[rnd() % 3];
+    while (s.size() < 40) s += ' ';
+    const uint8_t *p = reinterpret_cast<const uint8_t *>(s.data());
+    uint32_t w[4];
+    memcpy(w, p, 16);
+    auto at = [&](uint64_t i) -> uint32_t { return i < s.size() ? p[i] : 0u; };
+    bool ok = false;
+    const float v = wfloat32(w, tb, &ok);
+    if (ok) {
+      ++fast_f;
+      uint64_t e;
+      bool ne = false;
+      const float r = parse_float(at, 0, &e, &ne);
+      if (memcmp(&v, &r, 4)) {
+        if (bad++ < 10) printf("float mismatch '%.20s' fast=%.9g ref=%.9g\n", s.c_str(), v, r);
+      }
+    }
+    uint64_t iv = 0;
+    bool iok = false;
+    const bool pos = wuint32(w, tb, &iv, &iok);
+    if (iok) {
+      ++fast_i;
+      uint64_t r = 0;
+      const bool rpos = parse_uint(at, 0, false, &r);
+      if (pos != rpos || (pos && (uint32_t)iv != (uint32_t)r)) {
+        if (bad++ < 10) printf("uint mismatch '%.20s' fast=%llu ref=%llu\n", s.c_str(),
+                               (unsigned long long)iv, (unsigned long long)r);
+      }
+    }
+  }
+  printf("strings %ld, float fast %ld, uint fast %ld, mismatches %ld\n", n, fast_f, fast_i, bad);
+  return bad != 0;
+}

@@ -44,6 +44,7 @@ struct BlockCtx {
   Barrier bar{kThreads};
   Barrier wbar[kWaves] = {Barrier(kWave), Barrier(kWave), Barrier(kWave), Barrier(kWave)};
   unsigned char bal[kThreads];
+  uint32_t ws[kThreads];
   alignas(64) unsigned char scan[kThreads * 64];
   uint64_t mins[kThreads];
 };
@@ -62,6 +63,15 @@ struct HostBlock {
     for (int i = 0; i < kWave; ++i) m |= (uint64_t)(ctx->bal[w0 + i] != 0) << i;
     wave_sync();
     return m;
+  }
+  uint32_t wave_sum(uint32_t v) {
+    ctx->ws[t] = v;
+    wave_sync();
+    uint32_t r = 0;
+    const int w0 = t / kWave * kWave;
+    for (int i = 0; i < kWave; ++i) r += ctx->ws[w0 + i];
+    wave_sync();
+    return r;
   }
   uint64_t min_u64(uint64_t v) {
     ctx->mins[t] = v;
