@@ -25,6 +25,16 @@ DA_HD float u2f(uint32_t u) {
 #endif
 }
 
+DA_HD uint32_t f2u(float f) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __float_as_uint(f);
+#else
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  return u;
+#endif
+}
+
 DA_HD void atomic_or_u32(uint32_t *p, uint32_t v) {
 #if defined(__HIP_DEVICE_COMPILE__)
   atomicOr(p, v);

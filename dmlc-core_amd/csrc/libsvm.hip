@@ -23,7 +23,10 @@ __global__ void __launch_bounds__(kThreads) libsvm_tile(LibsvmArgs a) {
 }
 
 template <int MODE>
-__global__ void __launch_bounds__(kThreads) svm_fast_tile(FastSvmArgs a) {
+#ifndef FSVM_MINW
+#define FSVM_MINW 6  // workgroups per CU the fill kernel is register-budgeted for
+#endif
+__global__ void __launch_bounds__(kThreads, FSVM_MINW) svm_fast_tile(FastSvmArgs a) {
   __shared__ __attribute__((aligned(16))) fsvm::Shared sh;
   __shared__ uint64_t scratch[kBlockScratchU64];
   DevBlock bk{scratch};

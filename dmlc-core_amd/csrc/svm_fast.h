@@ -225,6 +225,32 @@ DA_HD SegOut segment_roles(const Tile &t, int tid) {
   return o;
 }
 
+// The exact byte decoders: rare on this path (exponents, runs that may cross
+// the 16-byte window or a chunk end, 9+ digit indices).
+// (Measured: out of line they cost more than the code size saves, so they
+// stay inline unless FSVM_OUTLINE_SLOW is defined.)
+#if defined(FSVM_OUTLINE_SLOW) && defined(__HIP_DEVICE_COMPILE__)
+#define FSVM_COLD __device__ __attribute__((noinline))
+#else
+#define FSVM_COLD DA_HD
+#endif
+// They read the text from global memory: no LDS pointer crosses the call.
+struct GSrc {  // text bytes; NUL at or beyond the chunk end (as Src)
+  const uint8_t *g;
+  uint64_t lim;
+  DA_HD uint32_t operator()(uint64_t p) const { return p < lim ? (uint32_t)g[p] : 0u; }
+};
+FSVM_COLD float slow_float(const uint8_t *text, uint64_t q, uint64_t lim) {
+  GSrc src{text, lim};
+  uint64_t e;
+  bool nan_err = false;
+  return parse_float(src, q, &e, &nan_err);
+}
+FSVM_COLD bool slow_uint(const uint8_t *text, uint64_t q, uint64_t lim, int wide, uint64_t *v) {
+  GSrc src{text, lim};
+  return parse_uint(src, q, wide != 0, v);
+}
+
 // MODE 1: count only (size query); MODE 2: parse and write.
 template <int MODE, class BK>
 DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk) {
@@ -289,11 +315,6 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk) {
   }
   // ---- first decode batch into registers (gives predecessors time to publish)
   const uint64_t P = t.tlo + (uint64_t)tid * kSegB;
-  Src src;
-  src.g = a.text;
-  src.wbase = t.tlo >= (uint64_t)kPre ? t.tlo - kPre : 0;
-  src.wend = mn<uint64_t>(t.thi + kPost, a.n);
-  src.lds = sh.c.text + (src.wbase + kPre - t.tlo);
   const bool one_chunk = sh.c.ncs == 0;  // no chunk boundary before cnext
   // the window decoders are exact when its 16 bytes belong to the run's chunk
   auto lim_of = [&](uint64_t q) { return one_chunk ? sh.c.cnext : t.next_cs(q); };
@@ -306,12 +327,7 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk) {
       const uint32_t w4[4] = {(uint32_t)wq.lo, (uint32_t)(wq.lo >> 32), (uint32_t)wq.hi, (uint32_t)(wq.hi >> 32)};
       v = wfloat32(w4, sh.dt, &ok);
     }
-    if (!ok) {
-      src.lim = lim;
-      uint64_t e;
-      bool nan_err = false;
-      v = parse_float(src, q, &e, &nan_err);
-    }
+    if (!ok) v = slow_float(a.text, q, lim);
     return v;
   };
   auto dec_index = [&](uint64_t q) -> uint64_t {
@@ -323,10 +339,7 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk) {
       const uint32_t w4[4] = {(uint32_t)wq.lo, (uint32_t)(wq.lo >> 32), (uint32_t)wq.hi, (uint32_t)(wq.hi >> 32)};
       pos = wuint32(w4, sh.dt, &v, &ok);
     }
-    if (!ok) {
-      src.lim = lim;
-      pos = parse_uint(src, q, a.wide != 0, &v);
-    }
+    if (!ok) pos = slow_uint(a.text, q, lim, a.wide, &v);
     if (!pos) {
       raise_error(a.err, E_NEG_INDEX, q);
       v = 0;
