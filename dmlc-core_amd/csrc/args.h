@@ -53,6 +53,28 @@ struct FastSvmArgs {
   uint64_t *res;        // dmlc_amd_result counts (written by the last tile)
 };
 
+// Single-pass uniform-grammar CSV kernel (csv_fast.h).
+struct FastCsvArgs {
+  const uint8_t *text;
+  uint64_t n;
+  const uint64_t *cs;
+  int nchunk;
+  uint32_t ntiles;
+  int wide;
+  uint32_t delim;
+  int skip_if_gated;
+  uint64_t *offset;
+  void *index;
+  float *value;
+  uint64_t cap[8];
+  uint64_t *chunk_tab;  // may be null
+  uint64_t *lb;
+  uint32_t *ticket;
+  uint32_t *gate;
+  unsigned long long *err;
+  uint64_t *res;
+};
+
 struct CsvArgs {
   const uint8_t *text;
   uint64_t n;
@@ -75,6 +97,7 @@ struct CsvArgs {
   uint64_t cap[8];
   uint64_t *chunk_tab;
   unsigned long long *err;
+  const uint32_t *gate;  // when set, the tile kernels run only if *gate != 0
 };
 
 }  // namespace dmlc_amd

@@ -242,7 +242,32 @@ int dmlc_amd_parse(const void *d_text, uint64_t nbytes, const uint64_t *d_chunk_
     for (int i = 0; i < 8; ++i) a.cap[i] = out->cap[i];
     a.chunk_tab = d_chunk_table ? d_chunk_table : chunk_sink;
     a.err = reinterpret_cast<unsigned long long *>(res + 8);
-    e = dmlc_amd::launch_csv(a, res, phase, s);
+    a.gate = ctl;
+    dmlc_amd::FastCsvArgs f;
+    std::memset(&f, 0, sizeof(f));
+    f.text = a.text;
+    f.n = nbytes;
+    f.cs = d_chunk_starts;
+    f.nchunk = nchunks;
+    f.ntiles = (uint32_t)nft;
+    f.wide = a.wide;
+    f.delim = a.delim;
+    f.skip_if_gated = phase == dmlc_amd::kPhaseFill;
+    f.offset = a.offset;
+    f.index = a.index;
+    f.value = reinterpret_cast<float *>(a.value);
+    for (int i = 0; i < 8; ++i) f.cap[i] = out->cap[i];
+    f.chunk_tab = d_chunk_table;
+    f.lb = lb;
+    f.ticket = ctl + 1;
+    f.gate = ctl;
+    f.err = ferr;
+    f.res = res;
+    // the uniform-grammar CSV kernel: float values, no label / weight column,
+    // a delimiter the number decoder cannot consume (csv_fast.h)
+    const bool use_fast = nbytes > 0 && prm->value_type == DMLC_AMD_F32 && prm->label_column < 0 &&
+                          prm->weight_column < 0 && a.fast_delim && !(prm->flags & DMLC_AMD_FLAG_EXACT);
+    e = dmlc_amd::launch_csv(a, f, use_fast, res, phase, s);
   } else {
     return DMLC_AMD_ERR_ARG;  // libfm: not built yet
   }

@@ -2,6 +2,7 @@
 // the tile body lives in csv_core.h.
 #include "block.h"
 #include "csv_core.h"
+#include "csv_fast.h"
 #include "dmlc_amd_kernels.h"
 #include "scan.h"
 
@@ -16,45 +17,83 @@ __global__ void __launch_bounds__(kThreads) csv_tile(CsvArgs a) {
   csv::tile<MODE>(a, sh, bk, blockIdx.x);
 }
 
-// fill phase after a count phase: the count phase's finalize turned "no error"
-// (~0) into 0; reopen it so the write pass can record the first error, and
-// store the closing offset (the reference's final push, libsvm_parser.h:157-159)
-// the size query could not (it had no output buffers)
-__global__ void reopen_kernel(uint64_t *res, uint64_t *offset, uint64_t cap_rows) {
+#ifndef FCSV_MINW
+#define FCSV_MINW 6
+#endif
+template <int MODE>
+__global__ void __launch_bounds__(kThreads, FCSV_MINW) csv_fast_tile(FastCsvArgs a) {
+  __shared__ __attribute__((aligned(16))) fcsv::Shared sh;
+  __shared__ uint64_t scratch[kBlockScratchU64];
+  DevBlock bk{scratch};
+  fcsv::tile<MODE>(a, sh, bk);
+}
+
+// fill phase after a count phase that fell back to the exact kernels: reopen
+// the first-error word so the write pass can record it, and store the closing
+// offset (the reference's final push) the size query could not
+__global__ void reopen_kernel(uint64_t *res, uint64_t *offset, uint64_t cap_rows, const uint32_t *gate) {
+  if (*gate == 0) return;
   if (res[8] == 0) res[8] = ~0ull;
   if (offset && res[0] < cap_rows + 1) offset[res[0]] = res[1];
 }
 
-__global__ void finalize_kernel(uint64_t *res) {
+// the error of whichever path produced the result
+__global__ void select_kernel(uint64_t *res, const uint32_t *gate, const unsigned long long *ferr) {
+  if (*gate == 0) res[8] = *ferr;
   if (res[8] == ~0ull) res[8] = 0;
-  res[9] = 1;  // dmlc_amd_result.path: exact tile kernels
+  res[9] = *gate;  // dmlc_amd_result.path
 }
 
 }  // namespace
 
-hipError_t launch_csv(const CsvArgs &a, uint64_t *res, int phase, hipStream_t s) {
+hipError_t launch_csv(const CsvArgs &a, const FastCsvArgs &f, bool use_fast, uint64_t *res, int phase,
+                      hipStream_t s) {
   hipError_t e;
+  uint32_t *gate = f.gate;
   if (phase != kPhaseFill) {
     if ((e = hipMemsetAsync(res, 0, 16 * sizeof(uint64_t), s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(res + 8, 0xFF, sizeof(uint64_t), s)) != hipSuccess) return e;
-  } else {
-    reopen_kernel<<<1, 1, 0, s>>>(res, a.offset, a.cap[C_ROWS]);
+    if ((e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(gate), use_fast ? 0 : 1, 1, s)) !=
+        hipSuccess)
+      return e;
   }
+  if (phase != kPhaseCount && f.chunk_tab &&
+      (e = hipMemsetAsync(f.chunk_tab, 0xFF, (size_t)f.nchunk * 8 * sizeof(uint64_t), s)) != hipSuccess)
+    return e;  // rows no tile writes are filled by chunk_fixup_kernel
+  if (use_fast) {
+    if ((e = hipMemsetAsync(f.ticket, 0, sizeof(uint32_t), s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(f.err, 0xFF, sizeof(uint64_t), s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(f.lb, 0, (size_t)f.ntiles * 8 * sizeof(uint64_t), s)) != hipSuccess) return e;
+    if (phase == kPhaseCount) {
+      prof_mark(0, s, "csv_fast_tile<1>");
+      csv_fast_tile<1><<<f.ntiles, kThreads, 0, s>>>(f);
+      prof_mark(1, s, "csv_fast_tile<1>");
+    } else {
+      prof_mark(0, s, "csv_fast_tile<2>");
+      csv_fast_tile<2><<<f.ntiles, kThreads, 0, s>>>(f);
+      prof_mark(1, s, "csv_fast_tile<2>");
+    }
+  } else if ((e = hipMemsetAsync(f.err, 0xFF, sizeof(uint64_t), s)) != hipSuccess) {
+    return e;
+  }
+  // ---- exact path, gated on the device flag (early exit when the fast path stood)
+  if (phase == kPhaseFill) reopen_kernel<<<1, 1, 0, s>>>(res, a.offset, a.cap[C_ROWS], gate);
   if (!a.ntiles && phase != kPhaseCount && a.offset && (e = hipMemsetAsync(a.offset, 0, 8, s)) != hipSuccess)
     return e;  // empty input: offset = {0}
   if (a.ntiles) {
     if (phase != kPhaseFill) {
       csv_tile<1><<<a.ntiles, kThreads, 0, s>>>(a);
       tile_scan_kernel<<<1, kThreads, 0, s>>>(a.tile_cnt, const_cast<uint64_t *>(a.tile_base), a.ntiles,
-                                              res, a.offset, a.cap[C_ROWS], nullptr);
+                                              res, a.offset, a.cap[C_ROWS], gate);
     }
     if (phase != kPhaseCount) {
-      prof_mark(0, s, "csv_tile<2>");
+      if (!use_fast) prof_mark(0, s, "csv_tile<2>");
       csv_tile<2><<<a.ntiles, kThreads, 0, s>>>(a);
-      prof_mark(1, s, "csv_tile<2>");
+      if (!use_fast) prof_mark(1, s, "csv_tile<2>");
     }
   }
-  finalize_kernel<<<1, 1, 0, s>>>(res);
+  select_kernel<<<1, 1, 0, s>>>(res, gate, f.err);
+  if (phase != kPhaseCount && f.chunk_tab && f.nchunk > 0) chunk_fixup_kernel<<<1, 1, 0, s>>>(f.chunk_tab, f.nchunk, res);
   return hipGetLastError();
 }
 

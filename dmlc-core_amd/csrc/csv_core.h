@@ -193,7 +193,15 @@ DA_HDF void walk(const CsvArgs &a, Src &src, const Seg &sg, uint32_t state, Cnt 
       in_line = true;
       col = 0;
       slow = (sg.slow >> i) & 1u;
-      if (MODE == 2 && x == a.cs[chunk]) {
+      // the chunk's first line: only newlines lie between its start and x
+      // (a chunk row is the exclusive count at the chunk start, dmlc_amd.h)
+      bool first = x == a.cs[chunk];
+      if (MODE == 2 && !first) {
+        uint64_t y = x;
+        while (y > a.cs[chunk] && is_nl(src(y - 1))) --y;
+        first = y == a.cs[chunk];
+      }
+      if (MODE == 2 && first) {
         uint64_t *row = a.chunk_tab + (uint64_t)chunk * 8;  // rows of 8 slots (dmlc_amd.h)
         for (int k = 0; k < C_N; ++k) row[k] = base.c[k] + cnt.c[k];
       }
@@ -292,6 +300,7 @@ template <int MODE, class BK>
 DA_HDF void tile(const CsvArgs &a, Shared &sh, BK &bk, uint64_t k) {
   const uint64_t tlo = k * a.tile_bytes;
   if (tlo >= a.n) return;
+  if (a.gate && *a.gate == 0) return;  // the uniform-grammar kernel handled this input
   const uint64_t thi = mn(tlo + a.tile_bytes, a.n);
   const int tid = bk.tid();
   const Cnt zero = cnt_zero();

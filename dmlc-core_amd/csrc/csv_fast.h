@@ -1,0 +1,354 @@
+// csv_fast.h -- the single-pass CSV tile body for the "uniform CSV grammar":
+// every byte is a number character (0-9 + - . e E), the delimiter or a
+// newline; no label / weight column; float values.  Inside that grammar
+// CSVParser::ParseBlock (src/data/csv_parser.h:71-149) reduces to:
+//
+//   row     a maximal run of non-newline bytes (leading newlines skipped,
+//           empty lines dropped, csv_parser.h:78-80,138-140); one offset each
+//   field   starts at a row start or after a delimiter that is not the last
+//           byte of the line (no phantom trailing field, :123-134)
+//   column  = delimiters between the row start and the field start
+//   token   a non-empty field: strtof consumed >= 1 byte, so the reference
+//           pushes value = ParseFloat(field), index = column (:112-118);
+//           an empty field only advances the column
+//
+// So the parse is bitmask arithmetic on 64-byte segments plus one segmented
+// count: the column of a token needs the delimiters since its row start,
+// which may lie in an earlier segment or tile -- a segmented scan inside the
+// tile and a segmented counter in the decoupled look-back across tiles.
+// Values use the 32-bit window decoder (fast_common.h wfloat32) with the
+// exact byte decoder as fallback.  Any byte outside the grammar sets the gate
+// word and the exact tile kernels (csv_core.h) produce the result.
+//
+// Same structure and block policy as svm_fast.h (the CPU emulator runs it).
+#pragma once
+#include "fast_common.h"
+
+namespace dmlc_amd {
+namespace fcsv {
+using namespace fast;
+
+// look-back slots: rows, values, the segmented delimiter tail, its row-start flag
+enum { Q_ROWS = 0, Q_VALS = 1, Q_TAIL = 2, Q_FLAG = 3 };
+
+struct Shared {  // LDS of one workgroup
+  TileCommon c;
+  uint64_t md[kThreads + 1];  // slot 0: the segment before the tile; slot t+1: segment t
+  uint64_t mn[kThreads + 1];
+  uint64_t ml[kThreads + 1];
+  uint32_t cls[256];  // byte classes: byte 0 number char, 1 outside the grammar, 2 newline, 3 delimiter
+  DecTables dt;
+  uint64_t segc;      // the tile's segmented carry (delimiters since the last row start before it)
+};
+
+DA_HD uint32_t class_of_csv(uint32_t b, uint32_t delim) {
+  if (b == delim) return 0x01000000u;
+  if (is_digitchar(b)) return 0x00000001u;
+  if (b == '\n' || b == '\r') return 0x00010000u;
+  return 0x00000100u;
+}
+
+// segmented sum on 32 bits: bit 31 = "a row starts here", bits 0-30 the
+// count since (a is the earlier operand)
+DA_HD uint32_t seg_combine(uint32_t a, uint32_t b) {
+  return (b >> 31) ? b : (a & 0x80000000u) | ((a + b) & 0x7FFFFFFFu);
+}
+// per-lane scan element: bits 0-15 rows, 16-31 values, 32-62 the segmented
+// delimiter count (seg_combine), 63 its flag
+struct CsvScanOp {
+  DA_HD uint64_t operator()(uint64_t a, uint64_t b) const {
+    const uint64_t lo = ((a & 0xFFFFFFFFull) + (b & 0xFFFFFFFFull)) & 0xFFFFFFFFull;
+    return lo | ((uint64_t)seg_combine((uint32_t)(a >> 32), (uint32_t)(b >> 32)) << 32);
+  }
+};
+
+// Look-back with the four slots above: rows and values are sums; the tail is
+// segmented (walking back, it stops at the nearest tile holding a row start).
+// Record word 0 = status | rows | values << 15 | tail << 30 | flag << 45;
+// words 1..3 = inclusive rows, values, and the carry out of the tile
+// (delimiters since its last row start, or through it).
+template <class BK>
+DA_HDF uint32_t csv_look_back(uint64_t *lb, uint32_t k, const uint32_t cnt[4], uint32_t *gate, TileCommon &c,
+                              BK &bk, uint64_t *segc) {
+  const uint32_t lane = bk.tid();
+  uint64_t j = k;
+  uint32_t spins = 0, rounds = 0;
+  uint64_t rows = 0, vals = 0, tail = 0;
+  bool seg_done = false;
+  bool done = k == 0;
+  while (!done) {
+    ++rounds;
+    uint64_t s = 0;
+    uint32_t st = 2;
+    if (lane < j) {
+      s = load_agent_u64(lb + (j - 1 - lane) * 8);
+      st = (uint32_t)(s >> 62);
+    }
+    const uint64_t zero = bk.ballot(st == 0), incl = bk.ballot(st == 2);
+    const uint32_t fz = zero ? (uint32_t)ctz64(zero) : 64u, fi = incl ? (uint32_t)ctz64(incl) : 64u;
+    const uint32_t tagg = fi < fz ? fi : fz;
+    const uint64_t mine = lane < tagg ? s : 0ull;
+    rows += bk.wave_sum((uint32_t)(mine & 0x7FFFu));
+    vals += bk.wave_sum((uint32_t)((mine >> 15) & 0x7FFFu));
+    if (!seg_done) {
+      const uint64_t flg = bk.ballot(lane < tagg && ((s >> 45) & 1u));
+      const uint32_t f = flg ? (uint32_t)ctz64(flg) : 64u;  // nearest tile with a row start
+      tail += bk.wave_sum(lane < tagg && lane <= f ? (uint32_t)((s >> 30) & 0x7FFFu) : 0u);
+      seg_done = f < 64u;
+    }
+    done = fi < fz;
+    if (done) {
+      if ((uint64_t)fi < j) {
+        if (lane == fi) {
+          const uint64_t *rec = lb + (j - 1 - fi) * 8;
+          for (int i = 0; i < 3; ++i) c.lbw[i] = load_agent_u64(const_cast<uint64_t *>(rec) + 1 + i);
+        }
+        bk.wave_sync();
+        rows += c.lbw[0];
+        vals += c.lbw[1];
+        if (!seg_done) tail += c.lbw[2];
+        bk.wave_sync();
+      }
+    } else {
+      j -= tagg;
+      if (tagg == 0) {
+        if (++spins > kSpinLimit) {
+          if (lane == 0) atomic_or_u32(gate, 2u);
+          done = true;
+        }
+        spin_pause();
+      }
+    }
+  }
+  if (lane == 0) {
+    c.base[Q_ROWS] = rows;
+    c.base[Q_VALS] = vals;
+    *segc = tail;
+  }
+  const uint64_t packed = (uint64_t)cnt[0] | ((uint64_t)cnt[1] << 15) | ((uint64_t)cnt[2] << 30) |
+                          ((uint64_t)cnt[3] << 45);
+  uint64_t *rec = lb + (uint64_t)k * 8;
+  if (lane < 3) {
+    const uint64_t v = lane == 0 ? rows + cnt[0] : lane == 1 ? vals + cnt[1]
+                                                           : (cnt[3] ? (uint64_t)cnt[2] : tail + cnt[2]);
+    store_agent_u64(rec + 1 + lane, v);
+  }
+  drain_stores();
+  bk.wave_sync();
+  if (lane == 0) store_agent_u64(rec, kSIncl | packed);
+  return rounds;
+}
+
+struct Tile {
+  const FastCsvArgs *a;
+  Shared *sh;
+  uint64_t tlo, thi;
+  DA_HD uint64_t next_cs(uint64_t p) const {  // first chunk start > p
+    for (uint32_t i = 0; i < sh->c.ncs; ++i)
+      if (sh->c.csl[i] > p) return sh->c.csl[i];
+    return sh->c.cnext;
+  }
+};
+
+// MODE 1: count only (size query); MODE 2: parse and write.
+template <int MODE, class BK>
+DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk) {
+  const int tid = bk.tid();
+  if (tid == 0) sh.c.tile = (a.skip_if_gated && *a.gate) ? ~0u : atomic_add_u32(a.ticket, 1);
+  bk.sync();
+  const uint32_t k = sh.c.tile;
+  if (k == ~0u) return;
+  Tile t;
+  t.a = &a;
+  t.sh = &sh;
+  t.tlo = (uint64_t)k * kTile;
+  t.thi = mn<uint64_t>(t.tlo + kTile, a.n);
+  if (tid == 0) {
+    chunk_list(a.cs, a.nchunk, t.tlo, t.thi, sh.c);
+    sh.md[0] = sh.mn[0] = sh.ml[0] = 0;
+  }
+  sh.cls[tid] = class_of_csv((uint32_t)tid, a.delim);
+  init_dec_tables(sh.dt, bk);
+  stage(a.text, a.n, t.tlo, sh.c, bk);
+  bk.sync();
+  // ---- classify: segment tid -> slot tid+1; lanes 0..15 also one dword
+  // each of the 64 bytes before the tile -> slot 0
+  uint32_t bad = 0;
+  {
+    const Masks m = classify64_lut(sh.c.text + kPre + tid * kSegB, sh.cls);
+    sh.md[tid + 1] = m.d;
+    sh.mn[tid + 1] = m.n;
+    sh.ml[tid + 1] = m.c;
+    // bytes past the end of the text are staged as blanks: judge valid bytes only
+    const uint64_t P0 = t.tlo + (uint64_t)tid * kSegB;
+    const uint64_t vmask = P0 >= a.n ? 0ull : (a.n - P0 >= 64 ? ~0ull : ((1ull << (a.n - P0)) - 1));
+    bad = (m.g & vmask) != 0;
+    if (tid < 16 && t.tlo > 0) {
+      uint32_t x;
+      memcpy(&x, sh.c.text + 4 * tid, 4);
+      const Nib b = classify_dword_lut(x, sh.cls);
+      atomic_or_u64(&sh.md[0], (uint64_t)b.d << (4 * tid));
+      atomic_or_u64(&sh.mn[0], (uint64_t)b.n << (4 * tid));
+      atomic_or_u64(&sh.ml[0], (uint64_t)b.c << (4 * tid));
+    }
+    if (tid == 0) bad |= sh.c.toomany;
+  }
+  bk.sync();
+  // ---- rows, fields, tokens of my segment
+  const uint64_t P = t.tlo + (uint64_t)tid * kSegB;
+  uint64_t RS = 0, T = 0, L = 0;
+  if (P < a.n) {
+    const int nv = (int)mn<uint64_t>(64, a.n - P);
+    const uint64_t valid = nv == 64 ? ~0ull : ((1ull << nv) - 1);
+    const uint64_t N = sh.mn[tid + 1];
+    L = sh.ml[tid + 1] & valid;
+    uint64_t S = 0;  // chunk starts: a "newline before" for the row rule, a field barrier
+    for (uint32_t i = 0; i < sh.c.ncs; ++i) {
+      const uint64_t x = sh.c.csl[i];
+      if (x >= P && x < P + (uint64_t)nv) S |= 1ull << (x - P);
+    }
+    const uint64_t nprev = (sh.mn[tid] >> 63) & 1u, lprev = (sh.ml[tid] >> 63) & 1u;
+    RS = ~N & valid & ((N << 1) | nprev | S);
+    const uint64_t FSd = ((L << 1) | lprev) & ~N & ~S & valid;
+    T = (RS | FSd) & sh.md[tid + 1];
+  }
+  if (bad) atomic_or_u32(&sh.c.bad, 1u);
+  // segmented delimiter count of my segment: since my last row start, or all
+  const uint32_t has_rs = RS != 0;
+  const uint32_t lastr = has_rs ? 63u - (uint32_t)clz64(RS) : 0u;
+  const uint32_t tailc = (uint32_t)popc64(has_rs ? (L & (~0ull << lastr)) : L);
+  const uint64_t mine = (uint64_t)popc64(RS) | ((uint64_t)popc64(T) << 16) | ((uint64_t)tailc << 32) |
+                        ((uint64_t)has_rs << 63);
+  uint64_t totp;
+  const uint64_t ex = bk.exclusive(mine, (uint64_t)0, CsvScanOp(), &totp);
+  const uint32_t nR = (uint32_t)(totp & 0xFFFF), nT = (uint32_t)((totp >> 16) & 0xFFFF);
+  const uint32_t cnt4[4] = {nR, nT, (uint32_t)((totp >> 32) & 0x7FFFFFFF), (uint32_t)(totp >> 63)};
+  if (tid == 0) {
+    uint64_t *rec = a.lb + (uint64_t)k * 8;
+    const uint64_t packed = (uint64_t)cnt4[0] | ((uint64_t)cnt4[1] << 15) | ((uint64_t)cnt4[2] << 30) |
+                            ((uint64_t)cnt4[3] << 45);
+    if (k == 0) {
+      store_agent_u64(rec + 1, cnt4[0]);
+      store_agent_u64(rec + 2, cnt4[1]);
+      store_agent_u64(rec + 3, cnt4[2]);
+      drain_stores();
+      store_agent_u64(rec, kSIncl | packed);
+    } else {
+      store_agent_u64(rec, kSAgg | packed);
+    }
+    if (sh.c.bad) atomic_or_u32(a.gate, 1u);
+  }
+  const bool one_chunk = sh.c.ncs == 0;
+  auto dec_float = [&](uint64_t q) -> float {
+    const uint64_t lim = one_chunk ? sh.c.cnext : t.next_cs(q);
+    bool ok = false;
+    float v = 0.f;
+    if (q + 16 <= lim) {
+      const W16 wq = win_at(sh.c.text, t.tlo, q);
+      const uint32_t w4[4] = {(uint32_t)wq.lo, (uint32_t)(wq.lo >> 32), (uint32_t)wq.hi, (uint32_t)(wq.hi >> 32)};
+      v = wfloat32(w4, sh.dt, &ok);
+    }
+    if (!ok) {
+      GSrc src{a.text, lim};
+      uint64_t e;
+      bool nan_err = false;
+      v = parse_float(src, q, &e, &nan_err);
+    }
+    return v;
+  };
+#ifndef FCSV_KB
+#define FCSV_KB 4
+#endif
+  constexpr int kB = FCSV_KB;  // tokens decoded before the look-back
+  float vb[kB > 0 ? kB : 1];
+  uint64_t mT = T;
+  if (MODE == 2) {
+#pragma unroll
+    for (int u = 0; u < kB; ++u) {
+      vb[u] = 0.f;
+      if (mT) {
+        vb[u] = dec_float(P + ctz64(mT));
+        mT &= mT - 1;
+      }
+    }
+  }
+  // ---- decoupled look-back by wave 0
+  if (tid < kWave) csv_look_back(a.lb, k, cnt4, a.gate, sh.c, bk, &sh.segc);
+  bk.sync();
+  const uint64_t bRows = sh.c.base[Q_ROWS], bVal = sh.c.base[Q_VALS], tcarry = sh.segc;
+  if (k + 1 == a.ntiles && tid == 0) {
+    const uint64_t rows = bRows + nR;
+    a.res[C_ROWS] = rows;
+    a.res[C_INDEX] = bVal + nT;
+    a.res[C_VALUE] = bVal + nT;
+    a.res[C_WEIGHT] = 0;
+    a.res[C_QID] = 0;
+    a.res[C_LABEL] = 0;
+    a.res[C_FIELD] = 0;
+    if (MODE == 2 && a.offset && rows < a.cap[C_ROWS] + 1) a.offset[rows] = bVal + nT;
+  }
+  if (MODE != 2) return;
+
+  // ---- stores: values and column indices, then row offsets
+  const uint64_t eR = bRows + (ex & 0xFFFF), eV = bVal + ((ex >> 16) & 0xFFFF);
+  const uint64_t sex = ex >> 32;  // segmented exclusive (flag in bit 31)
+  const uint64_t carry = (sex >> 31) ? (sex & 0x7FFFFFFFull) : tcarry + (sex & 0x7FFFFFFFull);
+  auto col_of = [&](uint32_t b) -> uint64_t {  // delimiters since the row start, token at bit b
+    const uint64_t below = (1ull << b) - 1;
+    const uint64_t r = RS & (below | (1ull << b));
+    if (r) return (uint64_t)popc64(L & below & (~0ull << (63 - clz64(r))));
+    return carry + popc64(L & below);
+  };
+  auto put = [&](uint64_t r, uint32_t b, float v) {
+    if (r < a.cap[C_VALUE] && r < a.cap[C_INDEX]) {
+      a.value[r] = v;
+      const uint64_t c = col_of(b);
+      if (a.wide) reinterpret_cast<uint64_t *>(a.index)[r] = c;
+      else reinterpret_cast<uint32_t *>(a.index)[r] = (uint32_t)c;
+    } else {
+      raise_error(a.err, E_CAPACITY, P + b);
+    }
+  };
+  {
+    uint64_t m = T;
+    uint64_t r = eV;
+#pragma unroll
+    for (int u = 0; u < kB; ++u) {
+      if (m) {
+        put(r, (uint32_t)ctz64(m), vb[u]);
+        m &= m - 1;
+        ++r;
+      }
+    }
+    for (; m; m &= m - 1, ++r) {
+      const uint32_t b = (uint32_t)ctz64(m);
+      put(r, b, dec_float(P + b));
+    }
+  }
+  {
+    uint64_t r = eR;
+    for (uint64_t m = RS; m; m &= m - 1, ++r) {
+      const int b = ctz64(m);
+      if (r < a.cap[C_ROWS]) a.offset[r] = eV + popc64(T & ((1ull << b) - 1));
+      else raise_error(a.err, E_CAPACITY, P + b);
+    }
+  }
+  // ---- per-chunk exclusive counts at each chunk start in my segment
+  if (a.chunk_tab) {
+    for (uint32_t i = 0; i < sh.c.ncs; ++i) {
+      const uint64_t x = sh.c.csl[i];
+      if (x < P || x >= P + kSegB || x >= t.thi) continue;
+      const uint64_t below = (1ull << (x - P)) - 1;
+      uint64_t *row = a.chunk_tab + (uint64_t)(sh.c.c_first + i) * 8;
+      row[C_ROWS] = eR + popc64(RS & below);
+      row[C_INDEX] = row[C_VALUE] = eV + popc64(T & below);
+      row[C_WEIGHT] = 0;
+      row[C_QID] = 0;
+      row[C_LABEL] = 0;
+      row[C_FIELD] = 0;
+    }
+  }
+}
+
+}  // namespace fcsv
+}  // namespace dmlc_amd

@@ -53,6 +53,7 @@ constexpr uint32_t kHiA = 0x09220050u, kHiB = 0x00040004u;  // HI[0..7]
 struct Masks {
   uint64_t d, n, c;
   uint32_t bad;
+  uint64_t g;  // table form: byte-1 plane (G digit for libsvm, outside-the-grammar for CSV)
 };
 
 DA_HD uint32_t nib_d(uint32_t cls) {  // digitchar byte flags -> 4 bits
@@ -179,6 +180,7 @@ DA_HD Masks classify64_lut(const uint8_t *p, const uint32_t *cls) {
   m.n = pn[0] | ((uint64_t)pn[1] << 32);
   m.c = pc[0] | ((uint64_t)pc[1] << 32);
   const uint64_t g = pg[0] | ((uint64_t)pg[1] << 32);
+  m.g = g;
   m.bad = (g & ~m.d) != 0;
   return m;
 }
@@ -448,6 +450,12 @@ DA_HD bool wuint32(const uint32_t w[4], const DecTables &tb, uint64_t *out, bool
   *out = (lead8(w, s, L) >> k) * tb.inv5[k];
   return true;
 }
+
+struct GSrc {  // text bytes; NUL at or beyond the chunk end (as Src), global memory
+  const uint8_t *g;
+  uint64_t lim;
+  DA_HD uint32_t operator()(uint64_t p) const { return p < lim ? (uint32_t)g[p] : 0u; }
+};
 
 // the 16 bytes at absolute position q (staged in LDS at `text`, which holds
 // position tlo - kPre at index 0; q < tile end) as a window

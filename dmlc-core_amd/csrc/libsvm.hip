@@ -64,6 +64,9 @@ hipError_t launch_libsvm(const LibsvmArgs &a, const FastSvmArgs &f, bool use_fas
         hipSuccess)
       return e;
   }
+  if (phase != kPhaseCount && f.chunk_tab &&
+      (e = hipMemsetAsync(f.chunk_tab, 0xFF, (size_t)f.nchunk * 8 * sizeof(uint64_t), s)) != hipSuccess)
+    return e;  // rows no tile writes are filled by chunk_fixup_kernel
   if (use_fast) {
     if ((e = hipMemsetAsync(f.ticket, 0, sizeof(uint32_t), s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(f.err, 0xFF, sizeof(uint64_t), s)) != hipSuccess) return e;
@@ -103,6 +106,7 @@ hipError_t launch_libsvm(const LibsvmArgs &a, const FastSvmArgs &f, bool use_fas
     }
   }
   select_kernel<<<1, 1, 0, s>>>(res, gate, f.err);
+  if (phase != kPhaseCount && f.chunk_tab && f.nchunk > 0) chunk_fixup_kernel<<<1, 1, 0, s>>>(f.chunk_tab, f.nchunk, res);
   return hipGetLastError();
 }
 

@@ -46,5 +46,19 @@ tile_scan_kernel(const uint64_t *tile_cnt, uint64_t *tile_base, uint32_t ntiles,
   }
 }
 
+// Chunk rows no tile wrote (chunks holding no line: all newlines, empty, or
+// starting at the end of the text) -- the launchers pre-fill the table with
+// ~0 -- take the exclusive counts of the next chunk, or the totals.
+__global__ void chunk_fixup_kernel(uint64_t *chunk_tab, int nchunk, const uint64_t *res) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  for (int c = nchunk - 1; c >= 0; --c) {
+    uint64_t *row = chunk_tab + (uint64_t)c * 8;
+    row[7] = 0;  // the unused eighth slot
+    if (row[0] != ~0ull) continue;
+    const uint64_t *nx = c + 1 < nchunk ? chunk_tab + (uint64_t)(c + 1) * 8 : res;
+    for (int i = 0; i < 8; ++i) row[i] = i < 7 ? nx[i] : 0;
+  }
+}
+
 }  // namespace
 }  // namespace dmlc_amd

@@ -235,11 +235,6 @@ DA_HD SegOut segment_roles(const Tile &t, int tid) {
 #define FSVM_COLD DA_HD
 #endif
 // They read the text from global memory: no LDS pointer crosses the call.
-struct GSrc {  // text bytes; NUL at or beyond the chunk end (as Src)
-  const uint8_t *g;
-  uint64_t lim;
-  DA_HD uint32_t operator()(uint64_t p) const { return p < lim ? (uint32_t)g[p] : 0u; }
-};
 FSVM_COLD float slow_float(const uint8_t *text, uint64_t q, uint64_t lim) {
   GSrc src{text, lim};
   uint64_t e;

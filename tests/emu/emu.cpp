@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "csv_core.h"
+#include "csv_fast.h"
 #include "dmlc_amd.h"
 #include "libsvm_core.h"
 #include "svm_fast.h"
@@ -120,6 +121,21 @@ void tile_scan(const std::vector<uint64_t> &cnt, std::vector<uint64_t> &base, ui
   for (int i = 0; i < C_N; ++i) res[i] = run[i];
 }
 
+// mirrors the launchers' chunk-table pre-fill and chunk_fixup_kernel (scan.h)
+void chunk_prefill(uint64_t *tab, int nchunk) {
+  if (tab) std::memset(tab, 0xFF, (size_t)(nchunk > 0 ? nchunk : 0) * 8 * sizeof(uint64_t));
+}
+void chunk_fixup(uint64_t *tab, int nchunk, const uint64_t *res) {
+  if (!tab) return;
+  for (int c = nchunk - 1; c >= 0; --c) {
+    uint64_t *row = tab + (uint64_t)c * 8;
+    row[7] = 0;
+    if (row[0] != ~0ull) continue;
+    const uint64_t *nx = c + 1 < nchunk ? tab + (uint64_t)(c + 1) * 8 : res;
+    for (int i = 0; i < 8; ++i) row[i] = i < 7 ? nx[i] : 0;
+  }
+}
+
 }  // namespace
 
 extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *cs, int nchunks,
@@ -134,6 +150,7 @@ extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *c
   std::vector<uint64_t> chunk_min(nchunks > 0 ? nchunks : 1, ~0ull), sink((nchunks > 0 ? nchunks : 1) * 8);
   unsigned long long *err = reinterpret_cast<unsigned long long *>(res + 8);
   if (!ntiles && !count_only && out->offset) out->offset[0] = 0;
+  if (!count_only) chunk_prefill(chunk_table, nchunks);
   if (prm->format == DMLC_AMD_LIBSVM) {
     // mirrors launch_libsvm (libsvm.hip): uniform-grammar kernel first, exact
     // tile kernels when it sets the gate (or indexing_mode < 0 / FLAG_EXACT)
@@ -245,6 +262,49 @@ extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *c
     for (int i = 0; i < 8; ++i) a.cap[i] = out->cap[i];
     a.chunk_tab = chunk_table ? chunk_table : sink.data();
     a.err = err;
+    // mirrors launch_csv (csv.hip): uniform-grammar kernel first, exact tile
+    // kernels when it sets the gate (or the parameters are outside its form)
+    const bool use_fast = nbytes > 0 && prm->value_type == DMLC_AMD_F32 && prm->label_column < 0 &&
+                          prm->weight_column < 0 && a.fast_delim && !(prm->flags & DMLC_AMD_FLAG_EXACT);
+    uint32_t gate = use_fast ? 0u : 1u, ticket = 0;
+    unsigned long long ferr = ~0ull;
+    if (use_fast) {
+      const uint64_t nft = (nbytes + fast::kTile - 1) / fast::kTile;
+      std::vector<uint64_t> lb(nft * 8 + 1, 0);
+      FastCsvArgs f;
+      std::memset(&f, 0, sizeof(f));
+      f.text = text;
+      f.n = nbytes;
+      f.cs = cs;
+      f.nchunk = nchunks;
+      f.ntiles = (uint32_t)nft;
+      f.wide = a.wide;
+      f.delim = a.delim;
+      f.offset = out->offset;
+      f.index = out->index;
+      f.value = reinterpret_cast<float *>(out->value);
+      for (int i = 0; i < 8; ++i) f.cap[i] = out->cap[i];
+      f.chunk_tab = chunk_table;
+      f.lb = lb.data();
+      f.ticket = &ticket;
+      f.gate = &gate;
+      f.err = &ferr;
+      f.res = res;
+      for (uint64_t k = 0; k < nft; ++k) {
+        fcsv::Shared *sh = new fcsv::Shared;
+        std::memset(sh, 0xCD, sizeof(*sh));
+        if (count_only) run_block([&](HostBlock &bk) { fcsv::tile<1>(f, *sh, bk); });
+        else run_block([&](HostBlock &bk) { fcsv::tile<2>(f, *sh, bk); });
+        delete sh;
+      }
+    }
+    std::fprintf(stderr, "emu: csv path=%s\n", gate ? "exact" : "fast");
+    if (!gate) {
+      res[8] = ferr;
+      if (res[8] == ~0ull) res[8] = 0;
+      if (!count_only) chunk_fixup(chunk_table, nchunks, res);
+      return 0;
+    }
     for (uint64_t k = 0; k < ntiles; ++k) {
       csv::Shared *sh = new csv::Shared;
       std::memset(sh, 0xCD, sizeof(*sh));
@@ -264,6 +324,7 @@ extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *c
     return DMLC_AMD_ERR_ARG;
   }
   if (res[8] == ~0ull) res[8] = 0;
+  if (!count_only) chunk_fixup(chunk_table, nchunks, res);
   return 0;
 }
 

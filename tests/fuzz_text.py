@@ -73,6 +73,40 @@ def uniform_libsvm(rng, nlines, maxfeat=40, violate=False):
     return text.encode("latin-1")
 
 
+def _csv_field(rng):
+    r = rng.random()
+    if r < 0.08:
+        return ""  # empty field: the column advances, nothing is pushed
+    if r < 0.75:
+        return "%.9g" % (rng.random() * 2 - 1)
+    return _NUM[int(rng.integers(0, len(_NUM)))]
+
+
+def uniform_csv(rng, nlines, maxcols=40, delim=",", violate=False):
+    """CSV in the grammar the single-pass CSV kernel handles (csv_fast.h):
+    number characters, the delimiter and newlines -- empty fields, trailing
+    delimiters, blank lines, CR/LF mixes, odd numbers.  violate=True also
+    injects bytes that send the input to the exact kernels."""
+    out = []
+    for _ in range(nlines):
+        r = rng.random()
+        if r < 0.04:
+            out.append("")
+            continue
+        ncol = int(rng.integers(1, maxcols + 1))
+        line = delim.join(_csv_field(rng) for _ in range(ncol))
+        if rng.random() < 0.05:
+            line += delim
+        if violate and rng.random() < 0.2:
+            line += rng.choice([" ", "\t1", "nan", "x", "\xef\xbb\xbf"])
+        out.append(line)
+    seps = ["\n"] * 12 + ["\r\n", "\r", "\n\n"]
+    text = "".join(line + seps[int(rng.integers(0, len(seps)))] for line in out)
+    if rng.random() < 0.3:
+        text = text.rstrip("\r\n")
+    return text.encode("latin-1")
+
+
 def random_cuts(rng, data, nmax=8, anywhere=False):
     """Chunk offsets: after a newline (as an InputSplit cuts), or, with
     anywhere=True, at arbitrary bytes (the C-ABI allows any chunking)."""

@@ -147,3 +147,25 @@ def test_emu_fast_equals_exact_synthetic():
     he = _emu_vs_oracle(data, offs, exact=True)
     assert hf["path"] == "fast" and he["path"] == "exact"
     assert hf["chunk_table"].tolist() == he["chunk_table"].tolist()
+
+
+def test_emu_csv_fast_fuzz_vs_oracle():
+    """Uniform-CSV inputs through the single-pass CSV tile body, one and
+    several tiles, odd chunkings: whichever path runs, the reference's result."""
+    rng = np.random.default_rng(606)
+    fast = 0
+    for it in range(40):
+        delim = ",;"[it % 2]
+        big = it % 8 == 7
+        data = fuzz_text.uniform_csv(rng, 900 if big else int(rng.integers(1, 30)),
+                                     120 if big else int(rng.integers(1, 30)), delim,
+                                     violate=(not big) and rng.random() < 0.25)
+        offs = fuzz_text.random_cuts(rng, data, 5, anywhere=rng.random() < 0.3)
+        o = po.parse_chunks(data, offs, fmt=po.CSV, delimiter=delim)
+        h = pyemu.parse(data, offs, "csv", delimiter=delim)
+        failed = check_fail(h, "csv", offs)
+        assert (o["status"] != 0) == failed, (it, data[:200], offs, o["msg"], h["error"])
+        if not failed:
+            assert diff(h, o) == [], (it, diff(h, o), offs)
+        fast += h["path"] == "fast"
+    assert fast > 20, fast

@@ -201,14 +201,15 @@ def test_gpu_empty_and_tiny(dm):
 import fuzz_text  # noqa: E402
 
 
-def _gpu_vs_oracle_paths(dm, data, offs, **kw):
+def _gpu_vs_oracle_paths(dm, data, offs, fmt=po.LIBSVM, **kw):
     """Default path and forced exact path both equal the oracle."""
-    o = po.parse_chunks(data, offs, fmt=po.LIBSVM, **kw)
+    o = po.parse_chunks(data, offs, fmt=fmt, **kw)
     res = {}
+    name = FMT_NAME[fmt]
     for exact in (False, True):
-        h = dm.parse_bytes(data, offs, fmt="libsvm", exact=exact, **kw)
+        h = dm.parse_bytes(data, offs, fmt=name, exact=exact, **kw)
         nch = len(offs) - 1
-        failed = bool(h["error"]) or (nch > 0 and dm.chunk_check(h, "libsvm", nch, h["counts"]) >= 0)
+        failed = bool(h["error"]) or (nch > 0 and dm.chunk_check(h, name, nch, h["counts"]) >= 0)
         assert (o["status"] != 0) == failed, (exact, o["msg"], h["error"], data[:200], offs, kw)
         if not failed:
             bad = diff(h, o)
@@ -287,3 +288,65 @@ def test_gpu_fast_equals_exact_bench_size(dm):
     assert bool((idx[:, 1:] > idx[:, :-1]).all())  # generator: strictly increasing ids
     v = outs[False]["value"]
     assert bool(((v >= 0) & (v < 1)).all())
+
+
+# ------------------------------------------------- single-pass CSV path --
+
+
+def test_gpu_csv_fast_fuzz_vs_oracle(dm):
+    rng = np.random.default_rng(8086)
+    paths = {"fast": 0, "exact": 0}
+    for it in range(300):
+        delim = ",;|"[it % 3]
+        data = fuzz_text.uniform_csv(rng, int(rng.integers(1, 40)), int(rng.integers(1, 40)), delim,
+                                     violate=rng.random() < 0.2)
+        offs = fuzz_text.random_cuts(rng, data, 6, anywhere=rng.random() < 0.3)
+        kw = {"delimiter": delim}
+        if rng.random() < 0.2:
+            kw["index_bits"] = 64
+        try:
+            paths[_gpu_vs_oracle_paths(dm, data, offs, fmt=po.CSV, **kw)["path"]] += 1
+        except AssertionError as e:
+            raise AssertionError("case %d: %s" % (it, e))
+    assert paths["fast"] > 150, paths
+
+
+def test_gpu_csv_fast_multi_tile_vs_oracle(dm):
+    """Rows and fields crossing 16 KiB tiles: the segmented column carry
+    through the look-back, long rows spanning several tiles."""
+    rng = np.random.default_rng(4242)
+    for it in range(16):
+        maxcols = [8, 60, 400, 3000][it % 4]
+        data = fuzz_text.uniform_csv(rng, int(rng.integers(100, 2000)) if maxcols < 3000 else 40, maxcols)
+        offs = fuzz_text.random_cuts(rng, data, int(rng.integers(0, 30)), anywhere=it % 3 == 1)
+        h = _gpu_vs_oracle_paths(dm, data, offs, fmt=po.CSV)
+        assert h["path"] == "fast", it
+
+
+def test_gpu_csv_fast_equals_exact_bench_size(dm):
+    """BASELINE config 3 (1M rows x 256 float columns): the single-pass CSV
+    kernel and the exact kernels agree bit for bit; CSR properties."""
+    import torch
+    text, _ = synth.rows(synth.CSV, 1 << 20, 256, seed=1)
+    starts = dm.text_chunk_starts(text)
+    d_text = torch.from_numpy(text).cuda()
+    d_cs = torch.from_numpy(starts).cuda()
+    outs = {}
+    for exact in (False, True):
+        p = dm.DeviceParser("csv", flags=dm.FLAG_EXACT if exact else 0)
+        out = p.parse(d_text, d_cs)
+        assert out["error"] == 0 and out["path"] == (1 if exact else 0)
+        outs[exact] = out
+    c = outs[False]["counts"]
+    assert c[:7] == outs[True]["counts"][:7]
+    assert c[dm.ROWS] == 1 << 20 and c[dm.INDEX] == 256 << 20 and c[dm.VALUE] == 256 << 20
+    for k in ("offset", "index", "value"):
+        a, b = outs[False][k], outs[True][k]
+        assert torch.equal(a.view(torch.int32) if a.dtype == torch.float32 else a,
+                           b.view(torch.int32) if b.dtype == torch.float32 else b), k
+    off = outs[False]["offset"]
+    assert bool((off[1:] - off[:-1] == 256).all())
+    idx = outs[False]["index"].view(-1, 256).to(torch.int64)
+    assert bool((idx == torch.arange(256, device=idx.device)).all())
+    v = outs[False]["value"]
+    assert bool(((v >= -1) & (v < 1)).all())
