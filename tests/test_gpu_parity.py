@@ -350,3 +350,21 @@ def test_gpu_csv_fast_equals_exact_bench_size(dm):
     assert bool((idx == torch.arange(256, device=idx.device)).all())
     v = outs[False]["value"]
     assert bool(((v >= -1) & (v < 1)).all())
+
+
+def test_gpu_sharded_parts_concat(dm):
+    """Each rank's byte range (dmlc_amd_dist.part_range: the reference's
+    ResetPartition split) parsed on the GPU and concatenated on the host with
+    offset rebasing equals one parse of the whole input (BASELINE config 5's
+    sharding, here sequentially on one device)."""
+    import dmlc_amd_dist as dd
+    for fmt, name in ((po.LIBSVM, "libsvm"), (po.CSV, "csv")):
+        text, _ = synth.rows(synth.LIBSVM if fmt == po.LIBSVM else synth.CSV, 40000, 64, seed=5)
+        data = text.tobytes()
+        whole = dm.parse_bytes(data, dm.text_chunk_starts(text).tolist(), fmt=name)
+        for world in (2, 8):
+            parts = [dd.parse_part(data, r, world, fmt=name, chunk_bytes=1 << 20) for r in range(world)]
+            assert all(p["error"] == 0 and p["path"] == "fast" for p in parts)
+            cat = dd.concat_csr(parts)
+            for k in ("offset", "index", "value"):
+                assert np.asarray(cat[k]).tobytes() == np.asarray(whole[k]).tobytes(), (name, world, k)
