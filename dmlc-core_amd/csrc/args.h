@@ -47,7 +47,6 @@ struct FastSvmArgs {
   uint64_t cap[8];
   uint64_t *chunk_tab;  // may be null
   uint64_t *lb;         // [ntiles][8] look-back records, zeroed per launch
-  uint32_t *ticket;     // tile ticket counter, zeroed per launch
   uint32_t *gate;       // != 0: input left the grammar -> exact path
   unsigned long long *err;  // first error of this path
   uint64_t *res;        // dmlc_amd_result counts (written by the last tile)
@@ -69,7 +68,6 @@ struct FastCsvArgs {
   uint64_t cap[8];
   uint64_t *chunk_tab;  // may be null
   uint64_t *lb;
-  uint32_t *ticket;
   uint32_t *gate;
   unsigned long long *err;
   uint64_t *res;

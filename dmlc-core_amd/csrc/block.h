@@ -20,6 +20,18 @@ struct DevBlock {
     __builtin_amdgcn_wave_barrier();
   }
 
+  // v of lane `src` of the calling wave (all lanes active)
+  template <typename T>
+  __device__ __forceinline__ static T shfl(T v, int src) {
+    static_assert(sizeof(T) % 4 == 0, "4-byte granular");
+    T o;
+    const int *s = reinterpret_cast<const int *>(&v);
+    int *d = reinterpret_cast<int *>(&o);
+#pragma unroll
+    for (int k = 0; k < (int)(sizeof(T) / 4); ++k) d[k] = __shfl(s[k], src, kWave);
+    return o;
+  }
+
   // sum over the 64 lanes of the calling wave (all lanes active)
   __device__ __forceinline__ uint32_t wave_sum(uint32_t v) const {
 #pragma unroll

@@ -158,7 +158,7 @@ int dmlc_amd_parse(const void *d_text, uint64_t nbytes, const uint64_t *d_chunk_
   uint64_t *chunk_min = cv.take<uint64_t>(nc);
   uint64_t *chunk_sink = cv.take<uint64_t>((size_t)nc * 8);
   const uint64_t nft = (nbytes + kFastTile - 1) / kFastTile;
-  uint32_t *ctl = cv.take<uint32_t>(4);               // gate, ticket
+  uint32_t *ctl = cv.take<uint32_t>(4);               // gate
   unsigned long long *ferr = cv.take<unsigned long long>(1);
   uint64_t *lb = cv.take<uint64_t>(nft * 8 + 1);
   if (!tile_cnt || !tile_base || !chunk_min || !chunk_sink || !ctl || !ferr || !lb) return DMLC_AMD_ERR_ARG;
@@ -211,7 +211,6 @@ int dmlc_amd_parse(const void *d_text, uint64_t nbytes, const uint64_t *d_chunk_
     for (int i = 0; i < 8; ++i) f.cap[i] = out->cap[i];
     f.chunk_tab = d_chunk_table;
     f.lb = lb;
-    f.ticket = ctl + 1;
     f.gate = ctl;
     f.err = ferr;
     f.res = res;
@@ -259,7 +258,6 @@ int dmlc_amd_parse(const void *d_text, uint64_t nbytes, const uint64_t *d_chunk_
     for (int i = 0; i < 8; ++i) f.cap[i] = out->cap[i];
     f.chunk_tab = d_chunk_table;
     f.lb = lb;
-    f.ticket = ctl + 1;
     f.gate = ctl;
     f.err = ferr;
     f.res = res;

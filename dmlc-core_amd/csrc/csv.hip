@@ -25,7 +25,7 @@ __global__ void __launch_bounds__(kThreads, FCSV_MINW) csv_fast_tile(FastCsvArgs
   __shared__ __attribute__((aligned(16))) fcsv::Shared sh;
   __shared__ uint64_t scratch[kBlockScratchU64];
   DevBlock bk{scratch};
-  fcsv::tile<MODE>(a, sh, bk);
+  fcsv::tile<MODE>(a, sh, bk, blockIdx.x);
 }
 
 // fill phase after a count phase that fell back to the exact kernels: reopen
@@ -61,7 +61,6 @@ hipError_t launch_csv(const CsvArgs &a, const FastCsvArgs &f, bool use_fast, uin
       (e = hipMemsetAsync(f.chunk_tab, 0xFF, (size_t)f.nchunk * 8 * sizeof(uint64_t), s)) != hipSuccess)
     return e;  // rows no tile writes are filled by chunk_fixup_kernel
   if (use_fast) {
-    if ((e = hipMemsetAsync(f.ticket, 0, sizeof(uint32_t), s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(f.err, 0xFF, sizeof(uint64_t), s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(f.lb, 0, (size_t)f.ntiles * 8 * sizeof(uint64_t), s)) != hipSuccess) return e;
     if (phase == kPhaseCount) {

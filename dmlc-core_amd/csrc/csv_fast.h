@@ -152,21 +152,25 @@ struct Tile {
 
 // MODE 1: count only (size query); MODE 2: parse and write.
 template <int MODE, class BK>
-DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk) {
+DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
+  // Tile k = workgroup k (its blockIdx).  The look-back needs every tile's
+  // predecessors to become resident eventually; workgroups are dispatched in
+  // index order on every XCD, so the least unstarted tile's XCD only holds
+  // lower tiles, which finish.  (A device-wide ticket counter gave the same
+  // guarantee for any dispatch order but saturates near 88 grabs/us -- it
+  // capped the 131k-tile launch at ~1.5 ms.)  Should a predecessor ever not
+  // publish, kSpinLimit bounds the wait and the exact kernels take over.
   const int tid = bk.tid();
-  if (tid == 0) sh.c.tile = (a.skip_if_gated && *a.gate) ? ~0u : atomic_add_u32(a.ticket, 1);
-  bk.sync();
-  const uint32_t k = sh.c.tile;
-  if (k == ~0u) return;
+  if (a.skip_if_gated && *a.gate) return;  // fill phase after an exact-path count: block-uniform
+  FAST_STAMP(k, 0);
+  FAST_STAMP(k, 1);
   Tile t;
   t.a = &a;
   t.sh = &sh;
   t.tlo = (uint64_t)k * kTile;
   t.thi = mn<uint64_t>(t.tlo + kTile, a.n);
-  if (tid == 0) {
-    chunk_list(a.cs, a.nchunk, t.tlo, t.thi, sh.c);
-    sh.md[0] = sh.mn[0] = sh.ml[0] = 0;
-  }
+  if (tid < kWave) chunk_list(a.cs, a.nchunk, t.tlo, t.thi, sh.c, bk);
+  if (tid == 0) sh.md[0] = sh.mn[0] = sh.ml[0] = 0;
   sh.cls[tid] = class_of_csv((uint32_t)tid, a.delim);
   init_dec_tables(sh.dt, bk);
   stage(a.text, a.n, t.tlo, sh.c, bk);

@@ -17,7 +17,10 @@ constexpr int kPost = 128;               // staged bytes after it (runs crossing
 constexpr int kStage = kPre + kTile + kPost;
 constexpr int kMaxCs = 32;               // chunk starts per tile the fast path accepts
 constexpr uint64_t kAgg = 1ull << 62, kIncl = 2ull << 62, kValMask = (1ull << 62) - 1;
-constexpr uint32_t kSpinLimit = 1u << 26;
+// look-back rounds without progress before a tile gives up and hands the
+// input to the exact kernels (never expected: a safety valve that bounds the
+// wait should a predecessor tile not be resident, see svm_fast.h tile order)
+constexpr uint32_t kSpinLimit = 1u << 22;
 
 // Diagnostic build only (-DDMLC_AMD_STAMPS, libdmlc_amd_stamps.so): thread 0
 // of each tile records s_memtime at phase boundaries into g_stamps; the
@@ -479,23 +482,54 @@ struct TileCommon {
   uint32_t ncs, c_first, tile, toomany, bad;
 };
 
-// Thread 0: the chunk starts touching [tlo, thi] (binary search once).
-DA_HD void chunk_list(const uint64_t *cs, int nchunk, uint64_t tlo, uint64_t thi, TileCommon &c) {
-  const int c0 = chunk_of(cs, nchunk, tlo);
-  c.cfloor = cs[c0];
-  int i = c0;
-  if (cs[i] < tlo) ++i;
-  c.c_first = (uint32_t)i;
-  uint32_t m = 0;
-  while (i < nchunk && cs[i] <= thi) {
-    if (m < kMaxCs) c.csl[m] = cs[i];
-    ++m;
-    ++i;
+// Wave 0 (all 64 lanes): the chunk starts touching [tlo, thi].  The chunk of
+// tlo is found by a 64-ary search -- one round of 64 independent loads per
+// factor of 64 chunks, instead of a dependent binary-search chain per tile
+// (9 loads at 257 chunks, the longest latency of the tile prologue) -- and the
+// list comes from one more window load: csl = cs[c_first ..] inside [tlo, thi]
+// (excluding cs[nchunk]), cnext = the entry after the list (cs[nchunk] == n).
+template <class BK>
+DA_HDF void chunk_list(const uint64_t *cs, int nchunk, uint64_t tlo, uint64_t thi, TileCommon &c,
+                       BK &bk) {
+  const uint32_t lane = (uint32_t)bk.tid();
+  const uint64_t kBig = ~0ull;
+  // invariant: cs[lo] <= tlo, the answer (last i < nchunk with cs[i] <= tlo) lies in [lo, lo + cnt)
+  uint64_t lo = 0, cnt = (uint64_t)nchunk;
+  while (cnt > (uint64_t)kWave) {
+    const uint64_t S = (cnt + kWave - 1) / kWave;
+    const uint64_t i = lo + lane * S;
+    const uint64_t v = (lane * S < cnt) ? cs[i] : kBig;
+    const uint64_t m = bk.ballot(v <= tlo);
+    const uint64_t j = 63 - clz64(m);  // lane 0 always holds (cs[lo] <= tlo)
+    const uint64_t nlo = lo + j * S;
+    cnt = mn<uint64_t>(S, lo + cnt - nlo);
+    lo = nlo;
   }
-  c.ncs = m < kMaxCs ? m : kMaxCs;
-  c.cnext = cs[i];  // cs[nchunk] == n
-  c.toomany = m > kMaxCs;
-  c.bad = 0;
+  // window cs[lo .. lo + 64) (entries past cs[nchunk] read as "beyond")
+  uint64_t v = lo + lane <= (uint64_t)nchunk ? cs[lo + lane] : kBig;
+  uint64_t m = bk.ballot(lane < cnt && v <= tlo);
+  const uint64_t c0 = lo + (63 - clz64(m));
+  if (c0 - lo > (uint64_t)(kWave - kMaxCs - 2)) {  // the list may run past the window: reload at c0
+    lo = c0;
+    v = lo + lane <= (uint64_t)nchunk ? cs[lo + lane] : kBig;
+  }
+  const uint64_t idx = lo + lane;
+  const uint64_t vf = bk.shfl(v, (int)(c0 - lo));  // cs[c0]
+  const uint32_t first = (uint32_t)(c0 - lo) + (vf < tlo ? 1u : 0u);  // lane of c_first
+  const uint64_t lm = bk.ballot(lane >= first && idx < (uint64_t)nchunk && v <= thi);
+  const uint32_t m_all = (uint32_t)popc64(lm);
+  const uint32_t ln = first + m_all;                                 // lane of cnext
+  const uint64_t vn = bk.shfl(v, (int)(ln < (uint32_t)kWave ? ln : 0u));
+  if (lane >= first && lane - first < (uint32_t)kMaxCs && ((lm >> lane) & 1u)) c.csl[lane - first] = v;
+  if (lane == 0) {
+    c.cfloor = vf;
+    c.c_first = (uint32_t)(lo + first);
+    const bool over = m_all > (uint32_t)kMaxCs || ln >= (uint32_t)kWave;
+    c.ncs = over ? (uint32_t)kMaxCs : m_all;
+    c.cnext = ln < (uint32_t)kWave ? vn : kBig;
+    c.toomany = over;
+    c.bad = 0;
+  }
 }
 
 // All threads: stage [tlo - kPre, tlo + kTile + kPost) into LDS with 16-byte

@@ -30,7 +30,7 @@ __global__ void __launch_bounds__(kThreads, FSVM_MINW) svm_fast_tile(FastSvmArgs
   __shared__ __attribute__((aligned(16))) fsvm::Shared sh;
   __shared__ uint64_t scratch[kBlockScratchU64];
   DevBlock bk{scratch};
-  fsvm::tile<MODE>(a, sh, bk);
+  fsvm::tile<MODE>(a, sh, bk, blockIdx.x);
 }
 
 // fill phase after a count phase that fell back to the exact kernels: the
@@ -68,7 +68,6 @@ hipError_t launch_libsvm(const LibsvmArgs &a, const FastSvmArgs &f, bool use_fas
       (e = hipMemsetAsync(f.chunk_tab, 0xFF, (size_t)f.nchunk * 8 * sizeof(uint64_t), s)) != hipSuccess)
     return e;  // rows no tile writes are filled by chunk_fixup_kernel
   if (use_fast) {
-    if ((e = hipMemsetAsync(f.ticket, 0, sizeof(uint32_t), s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(f.err, 0xFF, sizeof(uint64_t), s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(f.lb, 0, (size_t)f.ntiles * 8 * sizeof(uint64_t), s)) != hipSuccess) return e;
     if (phase == kPhaseCount) {

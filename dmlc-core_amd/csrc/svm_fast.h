@@ -248,12 +248,16 @@ FSVM_COLD bool slow_uint(const uint8_t *text, uint64_t q, uint64_t lim, int wide
 
 // MODE 1: count only (size query); MODE 2: parse and write.
 template <int MODE, class BK>
-DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk) {
+DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
+  // Tile k = workgroup k (its blockIdx).  The look-back needs every tile's
+  // predecessors to become resident eventually; workgroups are dispatched in
+  // index order on every XCD, so the least unstarted tile's XCD only holds
+  // lower tiles, which finish.  (A device-wide ticket counter gave the same
+  // guarantee for any dispatch order but saturates near 88 grabs/us -- it
+  // capped the 131k-tile launch at ~1.5 ms.)  Should a predecessor ever not
+  // publish, kSpinLimit bounds the wait and the exact kernels take over.
   const int tid = bk.tid();
-  if (tid == 0) sh.c.tile = (a.skip_if_gated && *a.gate) ? ~0u : atomic_add_u32(a.ticket, 1);
-  bk.sync();
-  const uint32_t k = sh.c.tile;
-  if (k == ~0u) return;
+  if (a.skip_if_gated && *a.gate) return;  // fill phase after an exact-path count: block-uniform
   FAST_STAMP(k, 0);
   FAST_STAMP(k, 1);
   Tile t;
@@ -261,10 +265,8 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk) {
   t.sh = &sh;
   t.tlo = (uint64_t)k * kTile;
   t.thi = mn<uint64_t>(t.tlo + kTile, a.n);
-  if (tid == 0) {
-    chunk_list(a.cs, a.nchunk, t.tlo, t.thi, sh.c);
-    sh.md[0] = sh.mn[0] = sh.mc[0] = 0;
-  }
+  if (tid < kWave) chunk_list(a.cs, a.nchunk, t.tlo, t.thi, sh.c, bk);
+  if (tid == 0) sh.md[0] = sh.mn[0] = sh.mc[0] = 0;
   sh.cls[tid] = class_of((uint32_t)tid);
   init_dec_tables(sh.dt, bk);
   stage(a.text, a.n, t.tlo, sh.c, bk);
@@ -291,6 +293,10 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk) {
   }
   bk.sync();
   FAST_STAMP(k, 3);
+#if defined(FSVM_ABL_STOP) && FSVM_ABL_STOP == 1  // timing ablation only: stage + classify
+  if (sh.md[tid + 1] == 0x123456789ull) a.res[15] = sh.mn[tid];
+  return;
+#endif
   // ---- roles, counts, eligibility
   const SegOut so = segment_roles(t, tid);
   if (so.bad | bad) atomic_or_u32(&sh.c.bad, 1u);
@@ -302,6 +308,10 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk) {
   FAST_STAMP(k, 4);
   const uint32_t nL = (uint32_t)(totp & 0xFFFF), nW = (uint32_t)((totp >> 16) & 0xFFFF),
                  nI = (uint32_t)((totp >> 32) & 0xFFFF), nV = (uint32_t)(totp >> 48);
+#if defined(FSVM_ABL_STOP) && FSVM_ABL_STOP == 2  // + roles + block scan
+  if (ex == 0x123456789ull) a.res[15] = totp;
+  return;
+#endif
   // ---- publish this tile's aggregate
   const uint32_t cnt4[4] = {nL, nI, nV, nW};  // look-back slots Q_ROWS, Q_INDEX, Q_VALUE, Q_WEIGHT
   if (tid == 0) {
@@ -314,6 +324,9 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk) {
   // the window decoders are exact when its 16 bytes belong to the run's chunk
   auto lim_of = [&](uint64_t q) { return one_chunk ? sh.c.cnext : t.next_cs(q); };
   auto dec_float = [&](uint64_t q) -> float {
+#ifdef FSVM_ABL_NODEC  // timing ablation only (tools/build_variants.sh), never shipped
+    return (float)(uint32_t)q;
+#endif
     const uint64_t lim = lim_of(q);
     bool ok = false;
     float v = 0.f;
@@ -326,6 +339,9 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk) {
     return v;
   };
   auto dec_index = [&](uint64_t q) -> uint64_t {
+#ifdef FSVM_ABL_NODEC
+    return q;
+#endif
     const uint64_t lim = lim_of(q);
     uint64_t v = 0;
     bool ok = false, pos = true;
@@ -376,6 +392,10 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk) {
   }
   bk.sync();
   FAST_STAMP(k, 5);
+#if defined(FSVM_ABL_STOP) && FSVM_ABL_STOP == 3  // + first decode batch + look-back
+  if (sh.c.base[0] == 0x123456789ull) a.res[15] = (uint64_t)ib[0] + (uint64_t)vb[0];
+  return;
+#endif
   const uint64_t bRows = sh.c.base[Q_ROWS], bIdx = sh.c.base[Q_INDEX], bVal = sh.c.base[Q_VALUE],
                  bW = sh.c.base[Q_WEIGHT];
   // ---- the last tile publishes the totals (dmlc_amd_result.count)
@@ -397,6 +417,10 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk) {
   const uint64_t eL = bRows + (ex & 0xFFFF), eW = bW + ((ex >> 16) & 0xFFFF),
                  eI = bIdx + ((ex >> 32) & 0xFFFF), eV = bVal + (ex >> 48);
   auto put_index = [&](uint64_t r, uint64_t v, uint64_t q) {
+#ifdef FSVM_ABL_NOSTORE  // timing ablation only
+    if (v == 0x123456789ull) a.res[15] = r;
+    return;
+#endif
     if (r < a.cap[C_INDEX]) {
       if (a.wide) reinterpret_cast<uint64_t *>(a.index)[r] = v;
       else reinterpret_cast<uint32_t *>(a.index)[r] = (uint32_t)v;
@@ -405,6 +429,10 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk) {
     }
   };
   auto put_value = [&](uint64_t r, float v, uint64_t q) {
+#ifdef FSVM_ABL_NOSTORE
+    if (v == 1234.5f) a.res[15] = r;
+    return;
+#endif
     if (r < a.cap[C_VALUE]) a.value[r] = v;
     else raise_error(a.err, E_CAPACITY, q);
   };

@@ -48,6 +48,7 @@ struct BlockCtx {
   uint32_t ws[kThreads];
   alignas(64) unsigned char scan[kThreads * 64];
   uint64_t mins[kThreads];
+  uint64_t sh8[kThreads];
 };
 
 struct HostBlock {
@@ -64,6 +65,16 @@ struct HostBlock {
     for (int i = 0; i < kWave; ++i) m |= (uint64_t)(ctx->bal[w0 + i] != 0) << i;
     wave_sync();
     return m;
+  }
+  template <typename T>
+  T shfl(T v, int src) {
+    static_assert(sizeof(T) <= 8, "shfl element");
+    std::memcpy(&ctx->sh8[t], &v, sizeof(T));
+    wave_sync();
+    T r;
+    std::memcpy(&r, &ctx->sh8[t / kWave * kWave + src], sizeof(T));
+    wave_sync();
+    return r;
   }
   uint32_t wave_sum(uint32_t v) {
     ctx->ws[t] = v;
@@ -156,7 +167,7 @@ extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *c
     // tile kernels when it sets the gate (or indexing_mode < 0 / FLAG_EXACT)
     const bool use_fast = nbytes > 0 && prm->indexing_mode >= 0 && !(prm->flags & DMLC_AMD_FLAG_EXACT);
     const uint64_t nft = (nbytes + fsvm::kTile - 1) / fsvm::kTile;
-    uint32_t gate = use_fast ? 0u : 1u, ticket = 0;
+    uint32_t gate = use_fast ? 0u : 1u;
     unsigned long long ferr = ~0ull;
     std::vector<uint64_t> lb(nft * 8 + 1, 0);
     LibsvmArgs a;
@@ -200,15 +211,14 @@ extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *c
       for (int i = 0; i < 8; ++i) f.cap[i] = out->cap[i];
       f.chunk_tab = chunk_table;
       f.lb = lb.data();
-      f.ticket = &ticket;
       f.gate = &gate;
       f.err = &ferr;
       f.res = res;
       for (uint64_t k = 0; k < nft; ++k) {
         fsvm::Shared *sh = new fsvm::Shared;
         std::memset(sh, 0xCD, sizeof(*sh));
-        if (count_only) run_block([&](HostBlock &bk) { fsvm::tile<1>(f, *sh, bk); });
-        else run_block([&](HostBlock &bk) { fsvm::tile<2>(f, *sh, bk); });
+        if (count_only) run_block([&](HostBlock &bk) { fsvm::tile<1>(f, *sh, bk, (uint32_t)k); });
+        else run_block([&](HostBlock &bk) { fsvm::tile<2>(f, *sh, bk, (uint32_t)k); });
         delete sh;
       }
     }
@@ -266,7 +276,7 @@ extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *c
     // kernels when it sets the gate (or the parameters are outside its form)
     const bool use_fast = nbytes > 0 && prm->value_type == DMLC_AMD_F32 && prm->label_column < 0 &&
                           prm->weight_column < 0 && a.fast_delim && !(prm->flags & DMLC_AMD_FLAG_EXACT);
-    uint32_t gate = use_fast ? 0u : 1u, ticket = 0;
+    uint32_t gate = use_fast ? 0u : 1u;
     unsigned long long ferr = ~0ull;
     if (use_fast) {
       const uint64_t nft = (nbytes + fast::kTile - 1) / fast::kTile;
@@ -286,15 +296,14 @@ extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *c
       for (int i = 0; i < 8; ++i) f.cap[i] = out->cap[i];
       f.chunk_tab = chunk_table;
       f.lb = lb.data();
-      f.ticket = &ticket;
       f.gate = &gate;
       f.err = &ferr;
       f.res = res;
       for (uint64_t k = 0; k < nft; ++k) {
         fcsv::Shared *sh = new fcsv::Shared;
         std::memset(sh, 0xCD, sizeof(*sh));
-        if (count_only) run_block([&](HostBlock &bk) { fcsv::tile<1>(f, *sh, bk); });
-        else run_block([&](HostBlock &bk) { fcsv::tile<2>(f, *sh, bk); });
+        if (count_only) run_block([&](HostBlock &bk) { fcsv::tile<1>(f, *sh, bk, (uint32_t)k); });
+        else run_block([&](HostBlock &bk) { fcsv::tile<2>(f, *sh, bk, (uint32_t)k); });
         delete sh;
       }
     }

@@ -169,3 +169,36 @@ def test_emu_csv_fast_fuzz_vs_oracle():
             assert diff(h, o) == [], (it, diff(h, o), offs)
         fast += h["path"] == "fast"
     assert fast > 20, fast
+
+
+def _many_chunks(rng, data, n_cuts, cluster):
+    """Chunk starts after newlines, n_cuts of them; plus a dense cluster (>32
+    starts inside one 16 KiB tile) so both the 64-ary chunk search (nchunk > 64,
+    fast_common.h chunk_list) and the too-many-chunks fallback are exercised."""
+    a = np.frombuffer(data, dtype=np.uint8)
+    nl = (np.flatnonzero(a == 10) + 1)
+    nl = nl[nl < len(data)]
+    cuts = set(rng.choice(nl, size=min(n_cuts, len(nl)), replace=False).tolist())
+    mid = nl[(nl > 20000) & (nl < 36000)][:40]  # a cluster in tiles 1-2
+    if cluster:
+        cuts |= set(mid.tolist())
+    return [0] + sorted(cuts) + [len(data)]
+
+
+def test_emu_fast_many_chunks():
+    rng = np.random.default_rng(91)
+    for fmt in ("libsvm", "csv"):
+        if fmt == "libsvm":
+            text, _ = synth.rows(synth.LIBSVM, 2500, 12, seed=3)
+        else:
+            text, _ = synth.rows(synth.CSV, 2000, 16, seed=3)
+        data = text.tobytes()
+        assert len(data) > 3 * 16384
+        for n_cuts, cluster in ((70, False), (300, False), (300, True)):
+            offs = _many_chunks(rng, data, n_cuts, cluster)
+            f = po.LIBSVM if fmt == "libsvm" else po.CSV
+            o = po.parse_chunks(data, offs, fmt=f)
+            h = pyemu.parse(data, offs, fmt)
+            assert o["status"] == 0 and not check_fail(h, fmt, offs)
+            assert diff(h, o) == [], (fmt, n_cuts, diff(h, o))
+            assert h["path"] == ("exact" if cluster else "fast"), (fmt, n_cuts, h["path"])

@@ -7,7 +7,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out
 mkdir -p $O
 cd $R
-echo "== pytest -m gpu" && timeout -k 10 900 python -m pytest tests -m gpu -x -v > $O/pytest_gpu_$TAG.log 2>&1 \
+echo "== pytest -m gpu" && timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/pytest_gpu_$TAG.log 2>&1 \
   && tail -3 $O/pytest_gpu_$TAG.log \
   && echo "== smoke" && timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke_$TAG.log 2>&1 \
   && cat $O/smoke_$TAG.log \

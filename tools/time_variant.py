@@ -1,0 +1,36 @@
+"""Time dmlc_amd_parse (full call, HBM-resident) for ablation variants without
+checking results: DMLC_AMD_LIB=<variant.so> python tools/time_variant.py [config].
+Diagnostic only; bench.py is the measured number."""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "dmlc-core_amd", "python")]
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import dmlc_amd  # noqa: E402
+from tools import synth  # noqa: E402
+
+fmt, rows, width = {"libsvm": ("libsvm", 1 << 20, 128), "csv": ("csv", 1 << 20, 256)}[
+    sys.argv[1] if len(sys.argv) > 1 else "libsvm"]
+text, _ = synth.rows(synth.LIBSVM if fmt == "libsvm" else synth.CSV, rows, width, seed=1)
+starts = dmlc_amd.text_chunk_starts(text)
+dev = torch.device("cuda", 0)
+d_text = torch.from_numpy(text).to(dev)
+d_starts = torch.from_numpy(starts).to(dev)
+p = dmlc_amd.DeviceParser(fmt)
+res = torch.zeros(16, dtype=torch.int64, device=dev)
+counts = p.count(d_text, d_starts, result=res)
+out = p.alloc(counts)
+out["_csr"] = p.csr_of(out)
+for _ in range(3):
+    p.parse_into(d_text, d_starts, out, res)
+torch.cuda.synchronize()
+dmlc_amd.profile_begin()
+for _ in range(10):
+    p.parse_into(d_text, d_starts, out, res)
+torch.cuda.synchronize()
+ms, n, name = dmlc_amd.profile_end()
+print("%s %s %.4f ms" % (os.path.basename(os.environ.get("DMLC_AMD_LIB", "default")), name, ms / max(n, 1)))
