@@ -272,6 +272,10 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
   stage(a.text, a.n, t.tlo, sh.c, bk);
   bk.sync();
   FAST_STAMP(k, 2);
+#if defined(FSVM_ABL_STOP) && FSVM_ABL_STOP == 0  // timing ablation only: stage
+  if (sh.c.text[tid] == 0xAB && sh.c.ncs == 7) a.res[15] = sh.c.cnext;
+  return;
+#endif
   // ---- classify: segment tid -> slot tid+1; lanes 0..15 also one word each
   // of the 64 bytes before the tile -> slot 0
   uint32_t bad = 0;
@@ -361,27 +365,39 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
 #ifndef FSVM_KB
 #define FSVM_KB 4
 #endif
-  constexpr int kB = FSVM_KB;  // runs per role decoded before the look-back
-  uint64_t ib[kB > 0 ? kB : 1];
-  float vb[kB > 0 ? kB : 1];
-  uint64_t mI = so.I, mV = so.V;
+  constexpr int kB = FSVM_KB;  // runs per decoder decoded before the look-back
+  static_assert(kB >= 1 && kB <= 5, "batch positions are packed 6 bits each");
+  // Values, labels and weights share the float decoder: one position-ordered
+  // stream of float runs per thread (a separate label pass cost every wave one
+  // more full float-decoder iteration for its ~2 labels).
+  uint64_t ib[kB];
+  float fb[kB];
+  uint32_t fpos = 0;  // bit positions of the batch's float runs, 6 bits each
+  uint64_t mI = so.I, mF = so.V | so.L | so.W;
   if (MODE == 2) {
 #pragma unroll
     for (int u = 0; u < kB; ++u) {
       ib[u] = 0;
-      vb[u] = 0.f;
+      fb[u] = 0.f;
       if (mI) {
         ib[u] = dec_index(P + ctz64(mI));
         mI &= mI - 1;
       }
-      if (mV) {
-        vb[u] = dec_float(P + ctz64(mV));
-        mV &= mV - 1;
+      if (mF) {
+        const uint32_t bpos = (uint32_t)ctz64(mF);
+        fb[u] = dec_float(P + bpos);
+        fpos |= bpos << (6 * u);
+        mF &= mF - 1;
       }
     }
   }
   // ---- decoupled look-back by wave 0 (fast_common.h)
+#ifdef FSVM_ABL_NOLB  // timing ablation only: no look-back (wrong bases)
+  if (tid < 4) sh.c.base[tid] = 0;
+  if (false) {
+#else
   if (tid < kWave) {
+#endif
     const uint32_t rounds =
         look_back(a.lb, k, cnt4, a.gate, sh.c, bk);
 #if defined(DMLC_AMD_STAMPS) && defined(__HIP_DEVICE_COMPILE__)
@@ -393,7 +409,7 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
   bk.sync();
   FAST_STAMP(k, 5);
 #if defined(FSVM_ABL_STOP) && FSVM_ABL_STOP == 3  // + first decode batch + look-back
-  if (sh.c.base[0] == 0x123456789ull) a.res[15] = (uint64_t)ib[0] + (uint64_t)vb[0];
+  if (sh.c.base[0] == 0x123456789ull) a.res[15] = (uint64_t)ib[0] + (uint64_t)fb[0];
   return;
 #endif
   const uint64_t bRows = sh.c.base[Q_ROWS], bIdx = sh.c.base[Q_INDEX], bVal = sh.c.base[Q_VALUE],
@@ -437,44 +453,38 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
     else raise_error(a.err, E_CAPACITY, q);
   };
   {
-    const uint32_t nIm = (uint32_t)popc64(so.I), nVm = (uint32_t)popc64(so.V);
+    const uint32_t nIm = (uint32_t)popc64(so.I), nFm = (uint32_t)popc64(so.V | so.L | so.W);
+    uint64_t rv = eV, rl = eL, rw = eW;  // this thread's running output ranks
+    auto put_float = [&](uint32_t bpos, float v) {
+      const uint64_t bit = 1ull << bpos, q = P + bpos;
+      if (so.V & bit) {
+        put_value(rv++, v, q);
+      } else if (so.L & bit) {
+        if (rl < a.cap[C_ROWS]) {
+          a.label[rl] = v;
+          a.offset[rl] = eI + popc64(so.I & (bit - 1));
+        } else {
+          raise_error(a.err, E_CAPACITY, q);
+        }
+        ++rl;
+      } else {
+        if (rw < a.cap[C_WEIGHT]) a.weight[rw] = v;
+        else raise_error(a.err, E_CAPACITY, q);
+        ++rw;
+      }
+    };
 #pragma unroll
     for (int u = 0; u < kB; ++u) {
       if ((uint32_t)u < nIm) put_index(eI + u, ib[u], P);
-      if ((uint32_t)u < nVm) put_value(eV + u, vb[u], P);
+      if ((uint32_t)u < nFm) put_float((fpos >> (6 * u)) & 63u, fb[u]);
     }
-    uint64_t r = eI + kB;
-    for (; mI; mI &= mI - 1, ++r) {
+    for (uint64_t r = eI + kB; mI; mI &= mI - 1, ++r) {
       const uint64_t q = P + ctz64(mI);
       put_index(r, dec_index(q), q);
     }
-    r = eV + kB;
-    for (; mV; mV &= mV - 1, ++r) {
-      const uint64_t q = P + ctz64(mV);
-      put_value(r, dec_float(q), q);
-    }
-  }
-  {
-    uint64_t r = eL;
-    for (uint64_t m = so.L; m; m &= m - 1, ++r) {
-      const int b = ctz64(m);
-      const uint64_t q = P + b;
-      const float v = dec_float(q);
-      if (r < a.cap[C_ROWS]) {
-        a.label[r] = v;
-        a.offset[r] = eI + popc64(so.I & ((1ull << b) - 1));
-      } else {
-        raise_error(a.err, E_CAPACITY, q);
-      }
-    }
-  }
-  {
-    uint64_t r = eW;
-    for (uint64_t m = so.W; m; m &= m - 1, ++r) {
-      const uint64_t q = P + ctz64(m);
-      const float v = dec_float(q);
-      if (r < a.cap[C_WEIGHT]) a.weight[r] = v;
-      else raise_error(a.err, E_CAPACITY, q);
+    for (; mF; mF &= mF - 1) {
+      const uint32_t bpos = (uint32_t)ctz64(mF);
+      put_float(bpos, dec_float(P + bpos));
     }
   }
   FAST_STAMP(k, 6);
