@@ -347,18 +347,33 @@ struct DecTables {
   double p10[16], i10[16];  // 10^k and RN(10^-k)
   uint32_t inv5[9];         // 5^-k mod 2^32
 };
+// The tables as compile-time constants (constant evaluation divides with
+// IEEE round-to-nearest, so i10[k] is the correctly rounded 10^-k); each tile
+// copies them to LDS with one load per lane instead of computing them.
+constexpr DecTables make_dec_tables() {
+  DecTables t{};
+  double p = 1.0;
+  for (int k = 0; k < 16; ++k) {
+    t.p10[k] = p;
+    t.i10[k] = 1.0 / p;
+    p *= 10.0;
+  }
+  uint32_t v = 1;
+  for (int k = 0; k < 9; ++k) {
+    t.inv5[k] = v;
+    v *= 0xCCCCCCCDu;  // 5^-1 mod 2^32
+  }
+  return t;
+}
+constexpr DecTables kDecTables = make_dec_tables();
 template <class BK>
 DA_HDF void init_dec_tables(DecTables &tb, BK &bk) {
   const int t = bk.tid();
   if (t < 16) {
-    double p = 1.0;
-    for (int i = 0; i < t; ++i) p *= 10.0;
-    tb.p10[t] = p;
-    tb.i10[t] = 1.0 / p;  // correctly rounded reciprocal (IEEE division)
+    tb.p10[t] = kDecTables.p10[t];
+    tb.i10[t] = kDecTables.i10[t];
   } else if (t < 25) {
-    uint32_t v = 1;
-    for (int i = 0; i < t - 16; ++i) v *= 0xCCCCCCCDu;  // 5^-1 mod 2^32
-    tb.inv5[t - 16] = v;
+    tb.inv5[t - 16] = kDecTables.inv5[t - 16];
   }
 }
 DA_HD uint32_t udot4(uint32_t a, uint32_t b, uint32_t c) {  // sum of the 4 byte products + c
@@ -478,7 +493,7 @@ struct TileCommon {
   alignas(16) uint8_t text[kStage];  // position p <-> text[p - tlo + kPre]
   uint64_t csl[kMaxCs + 1];           // chunk starts in [tlo, thi]
   uint64_t cfloor, cnext, base[4];    // last chunk start <= tlo, first beyond the list, output bases
-  uint64_t lbw[4 * kWave];            // look-back round: values per lane and counter
+  uint64_t lbw[4];                    // look-back: the inclusive prefix read by one lane
   uint32_t ncs, c_first, tile, toomany, bad;
 };
 
