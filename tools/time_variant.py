@@ -33,4 +33,6 @@ for _ in range(10):
     p.parse_into(d_text, d_starts, out, res)
 torch.cuda.synchronize()
 ms, n, name = dmlc_amd.profile_end()
-print("%s %s %.4f ms" % (os.path.basename(os.environ.get("DMLC_AMD_LIB", "default")), name, ms / max(n, 1)))
+r = res.cpu().numpy().view(np.uint64)
+print("%s %s %.4f ms path=%d err=%#x res15=%d" % (os.path.basename(os.environ.get("DMLC_AMD_LIB", "default")),
+                                                  name, ms / max(n, 1), int(r[9]), int(r[8]), int(r[15])))
