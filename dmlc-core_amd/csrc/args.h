@@ -29,6 +29,11 @@ struct LibsvmArgs {
   const uint32_t *gate;  // when set, the tile kernels run only if *gate != 0
 };
 
+// libfm exact tile kernels (libfm_core.h): the libsvm block plus field ids.
+struct LibfmArgs : LibsvmArgs {
+  void *field;  // IndexType, one per index
+};
+
 // Single-pass uniform-grammar libsvm kernel (svm_fast.h).
 struct FastSvmArgs {
   const uint8_t *text;

@@ -266,8 +266,30 @@ int dmlc_amd_parse(const void *d_text, uint64_t nbytes, const uint64_t *d_chunk_
     const bool use_fast = nbytes > 0 && prm->value_type == DMLC_AMD_F32 && prm->label_column < 0 &&
                           prm->weight_column < 0 && a.fast_delim && !(prm->flags & DMLC_AMD_FLAG_EXACT);
     e = dmlc_amd::launch_csv(a, f, use_fast, res, phase, s);
-  } else {
-    return DMLC_AMD_ERR_ARG;  // libfm: not built yet
+  } else {  // DMLC_AMD_LIBFM
+    dmlc_amd::LibfmArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.text = reinterpret_cast<const uint8_t *>(d_text);
+    a.n = nbytes;
+    a.cs = d_chunk_starts;
+    a.nchunk = nchunks;
+    a.tile_bytes = T;
+    a.ntiles = (uint32_t)ntiles;
+    a.wide = prm->index_bits == 64;
+    a.indexing_mode = prm->indexing_mode;
+    a.tile_cnt = tile_cnt;
+    a.tile_base = tile_base;
+    a.offset = out->offset;
+    a.label = reinterpret_cast<float *>(out->label);
+    a.weight = out->weight;
+    a.index = out->index;
+    a.field = out->field;
+    a.value = reinterpret_cast<float *>(out->value);
+    for (int i = 0; i < 8; ++i) a.cap[i] = out->cap[i];
+    a.chunk_tab = d_chunk_table ? d_chunk_table : chunk_sink;
+    a.chunk_min = chunk_min;
+    a.err = reinterpret_cast<unsigned long long *>(res + 8);
+    e = dmlc_amd::launch_libfm(a, res, phase, s);
   }
   g_last_hip = e;
   return e == hipSuccess ? DMLC_AMD_OK : DMLC_AMD_ERR_HIP;

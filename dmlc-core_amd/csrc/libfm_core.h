@@ -1,0 +1,373 @@
+// libfm_core.h -- the libfm tile body (LibFMParser::ParseBlock,
+// src/data/libfm_parser.h:67-144; ParsePair strtonum.h:667-703 for the head,
+// ParseTriple strtonum.h:718-772 for the features), written once against the
+// block policy BK {tid, sync, min_u64, exclusive} so the GPU kernel
+// (libfm.hip) and the test-only CPU emulator (tests/emu) run the same code.
+//
+// Decomposition: as libsvm_core.h (count -> scan -> write over tiles that own
+// the line starts in their byte range, 8 KiB LDS windows, the owner of a line
+// start parses its head and marks R1, the first feature run).  The feature
+// runs of a line then follow ParseTriple's grammar as a 4-state machine whose
+// per-segment transition functions compose in a block scan:
+//
+//   state  meaning (the role of the last run)      next run, gap's first non-blank
+//   PRE    head / nothing yet                        -> PRE (no role until R1)
+//   A      field  (ParseTriple v1)                   ':' -> B (index)   else -> A (field)
+//   B      index  (v2)                               ':' -> C (value)   else -> A (field)
+//   C      value  (v3)                               -> A (field)
+//
+// A field is emitted only when its index follows (r >= 2, libfm_parser.h:
+// 111-120): the pair is written when the index run is reached, the field run
+// found by scanning back over the gap.  A line ending in "v1:" / "v1:v2:"
+// makes ParseTriple decode v2 / v3 at the line end (reading past it, as the
+// reference does).  Every v1 is decoded by the reference, so a '-' field
+// raises the sign error even when the triple is dropped (strtonum.h:416).
+#pragma once
+#include "libsvm_core.h"
+
+namespace dmlc_amd {
+namespace fm {
+
+using svm::Seg;
+using svm::r1_bit;
+using svm::fn_apply;
+using svm::FnCompose;
+using svm::kIdentityFn;
+using svm::first_line_start;
+using svm::gap_fnb;
+
+enum : uint32_t { S_PRE = 0, S_A = 1, S_B = 2, S_C = 3 };
+// transition tables (entry i at bits 2i): gap's first non-blank is ':' or not
+constexpr uint32_t kTColon = S_PRE | (S_B << 2) | (S_C << 4) | (S_A << 6);
+constexpr uint32_t kTOther = S_PRE | (S_A << 2) | (S_A << 4) | (S_A << 6);
+constexpr uint32_t kAllA = 0x55u, kAllPre = 0x00u;
+
+struct Head {
+  uint64_t label, wpos, r1;
+  bool row, w;
+};
+
+// Head of the line starting at `ls` (libfm_parser.h:79-98: ParsePair<real_t,
+// real_t>, then ParseTriple's first skip to R1).  `lim`: chunk end.  No
+// comment or qid handling in this grammar.
+template <typename F>
+DA_HDF Head head_parse(const F &at, uint64_t ls, uint64_t lim) {
+  Head h;
+  h.label = h.wpos = h.r1 = kNone;
+  h.row = h.w = false;
+  auto eol = [&](uint64_t p) { return p >= lim || (p > ls && is_nl(at(p))); };
+  uint64_t p = ls;
+  while (!eol(p) && !is_digitchar(at(p))) ++p;
+  if (eol(p)) return h;
+  h.row = true;
+  h.label = p;
+  while (!eol(p) && is_digitchar(at(p))) ++p;
+  while (!eol(p) && is_blank(at(p))) ++p;
+  if (!eol(p) && at(p) == ':') {
+    ++p;
+    while (!eol(p) && !is_digitchar(at(p))) ++p;
+    h.w = true;
+    h.wpos = p;  // == line end for "label:" -- decoded there, as the reference does
+    while (!eol(p) && is_digitchar(at(p))) ++p;
+  }
+  while (!eol(p) && !is_digitchar(at(p))) ++p;
+  if (!eol(p)) h.r1 = p;
+  return h;
+}
+
+// start of the digitchar run that ends before the gap ending at x
+template <typename F>
+DA_HD uint64_t prev_run(const F &at, uint64_t x, uint64_t floor) {
+  while (x > floor && !is_digitchar(at(x - 1))) --x;
+  while (x > floor && is_digitchar(at(x - 1))) --x;
+  return x;
+}
+
+// Event walk over one segment.  MODE 0: compose the transition function into
+// st; MODE 1: count from concrete state st; MODE 2: count and emit.
+template <int MODE>
+DA_HDF void walk(const LibfmArgs &a, Src &src, const uint32_t *r1bits, uint64_t w0, const Seg &sg,
+                 uint32_t &st, Cnt &cnt, const Base64 &base) {
+  uint32_t ev = sg.rs | sg.ls | sg.le;
+  int chunk = sg.chunk;
+  uint64_t cfloor = a.cs[chunk], cend = a.cs[chunk + 1];
+  src.lim = cend;
+  // one (field, index) pair: decode, check signs, store / track the chunk minimum
+  auto pair = [&](uint64_t fpos, uint64_t ipos, uint64_t x) {
+    if (MODE == 2 || a.indexing_mode < 0) {
+      uint64_t fv, iv;
+      bool ok = parse_uint(src, fpos, a.wide != 0, &fv);
+      ok = parse_uint(src, ipos, a.wide != 0, &iv) && ok;
+      if (!ok) {
+        raise_error(a.err, E_NEG_INDEX, x);
+        fv = iv = 0;
+      }
+      if (MODE == 1) {
+        atomic_min_u64((unsigned long long *)&a.chunk_min[chunk], (unsigned long long)(fv < iv ? fv : iv));
+      } else {
+        if (a.indexing_mode > 0 || (a.indexing_mode < 0 && a.chunk_min[chunk] > 0)) {
+          --fv;
+          --iv;
+        }
+        const uint64_t r = base.c[C_INDEX] + cnt.c[C_INDEX];
+        if (r < a.cap[C_INDEX] && r < a.cap[C_FIELD]) {
+          if (a.wide) {
+            reinterpret_cast<uint64_t *>(a.index)[r] = iv;
+            reinterpret_cast<uint64_t *>(a.field)[r] = fv;
+          } else {
+            reinterpret_cast<uint32_t *>(a.index)[r] = (uint32_t)iv;
+            reinterpret_cast<uint32_t *>(a.field)[r] = (uint32_t)fv;
+          }
+        } else {
+          raise_error(a.err, E_CAPACITY, x);
+        }
+      }
+    }
+    cnt.c[C_INDEX]++;
+    cnt.c[C_FIELD]++;
+  };
+  auto value = [&](uint64_t vpos, uint64_t x) {
+    if (MODE == 2) {
+      const uint64_t r = base.c[C_VALUE] + cnt.c[C_VALUE];
+      bool nan_err = false;
+      uint64_t e;
+      const float v = parse_float(src, vpos, &e, &nan_err);
+      if (nan_err) raise_error(a.err, E_NAN_LITERAL, x);
+      if (r < a.cap[C_VALUE]) a.value[r] = v;
+      else raise_error(a.err, E_CAPACITY, x);
+    }
+    cnt.c[C_VALUE]++;
+  };
+  while (ev) {
+    const int i = ctz32(ev);
+    ev &= ev - 1;
+    const uint64_t x = sg.lo + i;
+    while (x >= cend) {  // entered the next chunk
+      ++chunk;
+      cfloor = a.cs[chunk];
+      cend = a.cs[chunk + 1];
+      src.lim = cend;
+    }
+    if ((sg.ls >> i) & 1u) {
+      if (MODE == 0) {
+        st = kAllPre;
+      } else {
+        st = S_PRE;
+        const bool l0 = x == cfloor;
+        const Head h = head_parse(src, x, cend);
+        if (MODE == 2 && l0) {
+          uint64_t *row = a.chunk_tab + (uint64_t)chunk * 8;  // rows of 8 slots (dmlc_amd.h)
+          for (int k = 0; k < C_N; ++k) row[k] = base.c[k] + cnt.c[k];
+        }
+        if (h.row) {
+          if (MODE == 2) {
+            const uint64_t r = base.c[C_ROWS] + cnt.c[C_ROWS];
+            bool nan_err = false;
+            uint64_t e;
+            if (r < a.cap[C_ROWS]) {
+              a.label[r] = parse_float(src, h.label, &e, &nan_err);
+              a.offset[r] = base.c[C_INDEX] + cnt.c[C_INDEX];
+            } else {
+              raise_error(a.err, E_CAPACITY, x);
+            }
+            if (h.w) {
+              const uint64_t wr = base.c[C_WEIGHT] + cnt.c[C_WEIGHT];
+              if (wr < a.cap[C_WEIGHT]) a.weight[wr] = parse_float(src, h.wpos, &e, &nan_err);
+              else raise_error(a.err, E_CAPACITY, x);
+            }
+            if (nan_err) raise_error(a.err, E_NAN_LITERAL, x);
+          }
+          cnt.c[C_ROWS]++;
+          cnt.c[C_LABEL]++;
+          cnt.c[C_WEIGHT] += h.w;
+        }
+      }
+    }
+    if ((sg.rs >> i) & 1u) {
+      if (MODE == 0) {
+        if (r1_bit(r1bits, w0, x)) {
+          st = kAllA;
+        } else if (st != kAllPre) {
+          st = fn_apply(st, gap_fnb(src, x, cfloor) == ':' ? kTColon : kTOther);
+        }
+      } else {
+        uint32_t role = S_PRE;
+        if (r1_bit(r1bits, w0, x)) {
+          role = S_A;
+        } else if (st != S_PRE) {
+          const bool colon = gap_fnb(src, x, cfloor) == ':';
+          role = (st == S_A && colon) ? S_B : (st == S_B && colon) ? S_C : S_A;
+        }
+        if (role != S_PRE) st = role;
+        if (role == S_A) {  // v1 of a triple: the reference decodes it even if dropped
+          if (MODE == 2) {
+            uint64_t v;
+            if (!parse_uint(src, x, a.wide != 0, &v)) raise_error(a.err, E_NEG_INDEX, x);
+          }
+        } else if (role == S_B) {
+          pair(prev_run(src, x, cfloor), x, x);
+        } else if (role == S_C) {
+          value(x, x);
+        }
+      }
+    }
+    if (MODE != 0 && ((sg.le >> i) & 1u) && (st == S_A || st == S_B)) {
+      // "v1:" / "v1:v2:" at the line end: ParseTriple decodes at lend
+      if (gap_fnb(src, x + 1, cfloor) == ':') {
+        if (st == S_A) pair(prev_run(src, x + 1, cfloor), x + 1, x);
+        else value(x + 1, x);
+      }
+    }
+  }
+}
+
+// The tile body.  MODE 1 = count pass, MODE 2 = write pass.
+template <int MODE, class BK>
+DA_HDF void tile(const LibfmArgs &a, svm::Shared &sh, BK &bk, uint64_t k) {
+  const uint64_t tlo = k * a.tile_bytes;
+  if (tlo >= a.n) return;
+  const uint64_t thi = mn(tlo + a.tile_bytes, a.n);
+  const int tid = bk.tid();
+  const Cnt zero = cnt_zero();
+  Cnt tot = zero;   // totals of this tile's previous windows (block-uniform)
+  Cnt mine = zero;  // count pass: this thread's totals over all windows
+  Base64 tbase;
+  for (int i = 0; i < C_N; ++i) tbase.c[i] = MODE == 2 ? a.tile_base[k * C_N + i] : 0;
+
+  uint64_t w0 = first_line_start(a, bk, tlo, a.n);
+  if (w0 == kNone || w0 >= thi) {
+    if (MODE == 1 && tid < C_N) a.tile_cnt[k * C_N + tid] = 0;
+    return;
+  }
+  if (tid == 0) sh.pending[1] = kNone;
+  bk.sync();
+  int j = 0;             // window counter
+  uint32_t st0 = S_PRE;  // concrete state at the window start
+  bool done = false;
+  Src src;
+  src.g = a.text;
+  src.lds = sh.win;
+  while (!done) {
+    const uint64_t pend = sh.pending[(j + 1) & 1];  // written during window j-1
+    uint64_t wend = mn(w0 + (uint64_t)kWin, a.n);
+    if (wend == a.n) done = true;
+    if (wend > thi) {
+      const uint64_t e = first_line_start(a, bk, mx(w0, thi), wend);
+      if (e != kNone) {
+        wend = e;
+        done = true;
+      }
+    }
+    if (wend == w0) break;
+    if (tid == 0) sh.pending[j & 1] = (pend != kNone && pend >= wend) ? pend : kNone;
+    const uint64_t abase = w0 & ~15ull;
+    const uint64_t nunits = (wend - abase + 15) >> 4;
+    for (uint64_t u = tid; u < nunits; u += kThreads) {
+      const uint64_t g = abase + (u << 4);
+      if (g + 16 <= a.n) {
+        for (int q = 0; q < 4; ++q)
+          reinterpret_cast<uint32_t *>(&sh.win[u << 4])[q] = reinterpret_cast<const uint32_t *>(a.text + g)[q];
+      } else {
+        for (int q = 0; q < 16; ++q) sh.win[(u << 4) + q] = g + q < a.n ? a.text[g + q] : 0;
+      }
+    }
+    for (int i = tid; i < kWin / 32 + 1; i += kThreads) sh.r1bits[i] = 0;
+    bk.sync();
+    src.wbase = abase;
+    src.wend = mn(abase + (nunits << 4), a.n);
+    if (tid == 0 && pend != kNone && pend < wend)
+      atomic_or_u32(&sh.r1bits[(pend - w0) >> 5], 1u << ((pend - w0) & 31));
+
+    // ---- this thread's segment masks (libsvm_core.h)
+    Seg sg;
+    sg.lo = w0 + (uint64_t)tid * kSeg;
+    sg.hi = mn(sg.lo + (uint64_t)kSeg, wend);
+    sg.rs = sg.ls = sg.le = 0;
+    sg.chunk = 0;
+    if (sg.lo < sg.hi) {
+      sg.chunk = chunk_of(a.cs, a.nchunk, sg.lo);
+      src.lim = a.cs[sg.chunk + 1];
+      uint32_t dm = 0, nl = 0, csm = 0;
+      const int len = (int)(sg.hi - sg.lo);
+      for (int i = 0; i < len; ++i) {
+        const uint32_t c = sh.win[sg.lo + i - abase];
+        dm |= (uint32_t)is_digitchar(c) << i;
+        nl |= (uint32_t)is_nl(c) << i;
+      }
+      for (int c = sg.chunk; c < a.nchunk && a.cs[c] < sg.hi; ++c)
+        if (a.cs[c] >= sg.lo) csm |= 1u << (a.cs[c] - sg.lo);
+      const uint32_t prev = (sg.lo > 0 && !(csm & 1u) && is_digitchar(src(sg.lo - 1))) ? 1u : 0u;
+      sg.rs = (dm & ~((dm << 1) | prev)) | (csm & dm);
+      sg.ls = nl | csm;
+      bool nxt = sg.hi == a.n;
+      if (!nxt) {
+        const uint64_t h = sg.hi;
+        nxt = is_nl(h < src.wend ? sh.win[h - abase] : a.text[h]) || is_chunk_start(a.cs, a.nchunk, h);
+      }
+      sg.le = (sg.ls >> 1) | ((uint32_t)nxt << (len - 1));
+    }
+
+    // ---- head sections -> R1 marks
+    if (sg.ls) {
+      uint32_t m = sg.ls;
+      int chunk = sg.chunk;
+      while (m) {
+        const int i = ctz32(m);
+        m &= m - 1;
+        const uint64_t x = sg.lo + i;
+        while (x >= a.cs[chunk + 1]) ++chunk;
+        src.lim = a.cs[chunk + 1];
+        const Head h = head_parse(src, x, a.cs[chunk + 1]);
+        if (h.r1 != kNone) {
+          if (h.r1 < wend) atomic_or_u32(&sh.r1bits[(h.r1 - w0) >> 5], 1u << ((h.r1 - w0) & 31));
+          else sh.pending[j & 1] = h.r1;  // only the window's last line can get here
+        }
+      }
+    }
+    bk.sync();
+
+    // ---- transition function of my segment, then block scan
+    uint32_t fn = kIdentityFn;
+    Cnt dummy = zero;
+    Base64 nob;
+    for (int i = 0; i < C_N; ++i) nob.c[i] = 0;
+    if (sg.lo < sg.hi) walk<0>(a, src, sh.r1bits, w0, sg, fn, dummy, nob);
+    uint32_t fn_total;
+    const uint32_t fn_ex = bk.exclusive(fn, kIdentityFn, FnCompose(), &fn_total);
+    const uint32_t st = (fn_ex >> (2 * st0)) & 3u;
+    const uint32_t st_next = (fn_total >> (2 * st0)) & 3u;
+
+    // ---- count walk, then (write pass) scan + emit walk
+    Cnt c = zero;
+    if (sg.lo < sg.hi) {
+      uint32_t s2 = st;
+      walk<1>(a, src, sh.r1bits, w0, sg, s2, c, nob);
+    }
+    if (MODE == 1) {
+      mine = CntAdd()(mine, c);
+    } else {
+      Cnt wtot;
+      const Cnt ex = bk.exclusive(c, zero, CntAdd(), &wtot);
+      if (sg.lo < sg.hi) {
+        Base64 b;
+        for (int i = 0; i < C_N; ++i) b.c[i] = tbase.c[i] + tot.c[i] + ex.c[i];
+        Cnt local = zero;
+        uint32_t s3 = st;
+        walk<2>(a, src, sh.r1bits, w0, sg, s3, local, b);
+      }
+      tot = CntAdd()(tot, wtot);
+    }
+    st0 = st_next;
+    w0 = wend;
+    ++j;
+    bk.sync();
+  }
+  if (MODE == 1) {
+    Cnt total;
+    (void)bk.exclusive(mine, zero, CntAdd(), &total);
+    if (tid < C_N) a.tile_cnt[k * C_N + tid] = total.c[tid];
+  }
+}
+
+}  // namespace fm
+}  // namespace dmlc_amd

@@ -138,12 +138,14 @@ class HipParser : public dmlc::Parser<IndexType, DType> {
       prm_.format = DMLC_AMD_LIBSVM;
     } else if (fmt == "csv") {
       prm_.format = DMLC_AMD_CSV;
+    } else if (fmt == "libfm") {  // data.cc:206-209
+      prm_.format = DMLC_AMD_LIBFM;
     } else {
       throw dmlc::Error("Unknown data type " + fmt);
     }
     for (const auto &kv : spec_.args) {  // LibSVMParserParam / CSVParserParam fields
       if (kv.first == "format") continue;
-      if (prm_.format == DMLC_AMD_LIBSVM && kv.first == "indexing_mode") {
+      if ((prm_.format == DMLC_AMD_LIBSVM || prm_.format == DMLC_AMD_LIBFM) && kv.first == "indexing_mode") {
         prm_.indexing_mode = parse_int_arg(kv.first, kv.second);
       } else if (prm_.format == DMLC_AMD_CSV && kv.first == "label_column") {
         prm_.label_column = parse_int_arg(kv.first, kv.second);
@@ -160,8 +162,8 @@ class HipParser : public dmlc::Parser<IndexType, DType> {
       throw dmlc::Error("Check failed: label_column != weight_column");
     if (sizeof(DType) == 4 && !std::is_same<DType, float>::value) prm_.value_type = DMLC_AMD_I32;
     if (sizeof(DType) == 8) prm_.value_type = DMLC_AMD_I64;
-    if (prm_.format == DMLC_AMD_LIBSVM && prm_.value_type != DMLC_AMD_F32)
-      throw dmlc::Error("libsvm parser supports float values only");
+    if (prm_.format != DMLC_AMD_CSV && prm_.value_type != DMLC_AMD_F32)
+      throw dmlc::Error("libsvm / libfm parsers support float values only");
     if (const char *b = std::getenv("DMLC_AMD_BATCH_BYTES")) batch_bytes_ = std::strtoull(b, nullptr, 10);
     hip_check(hipGetDevice(&device_), "hipGetDevice");
     hip_check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
@@ -313,6 +315,7 @@ class HipParser : public dmlc::Parser<IndexType, DType> {
     out.weight = static_cast<float *>(d_weight_.get((c[DMLC_AMD_WEIGHT] + 1) * 4));
     out.qid = static_cast<uint64_t *>(d_qid_.get((c[DMLC_AMD_QID] + 1) * 8));
     out.index = d_index_.get((c[DMLC_AMD_INDEX] + 1) * isz);
+    out.field = d_field_.get((c[DMLC_AMD_FIELD] + 1) * isz);
     out.value = d_value_.get((c[DMLC_AMD_VALUE] + 1) * vsz);
     for (int i = 0; i < 7; ++i) out.cap[i] = c[i];
     p.flags = DMLC_AMD_FLAG_FILL_ONLY;
@@ -324,6 +327,7 @@ class HipParser : public dmlc::Parser<IndexType, DType> {
     h_weight_.reserve(c[DMLC_AMD_WEIGHT] + 1);
     h_qid_.reserve(c[DMLC_AMD_QID] + 1);
     h_index_.reserve((c[DMLC_AMD_INDEX] + 1) * isz);
+    h_field_.reserve((c[DMLC_AMD_FIELD] + 1) * isz);
     h_value_.reserve((c[DMLC_AMD_VALUE] + 1) * vsz);
     h_tab_.reserve((size_t)nchunks * 8);
     auto d2h = [&](void *dst, const void *src, size_t bytes) {
@@ -334,6 +338,7 @@ class HipParser : public dmlc::Parser<IndexType, DType> {
     d2h(h_weight_.p, out.weight, c[DMLC_AMD_WEIGHT] * 4);
     d2h(h_qid_.p, out.qid, c[DMLC_AMD_QID] * 8);
     d2h(h_index_.p, out.index, c[DMLC_AMD_INDEX] * isz);
+    d2h(h_field_.p, out.field, c[DMLC_AMD_FIELD] * isz);
     d2h(h_value_.p, out.value, c[DMLC_AMD_VALUE] * vsz);
     d2h(h_tab_.p, d_tab, (size_t)nchunks * 64);
     d2h(&res, d_res, sizeof(res));
@@ -355,6 +360,9 @@ class HipParser : public dmlc::Parser<IndexType, DType> {
       const uint64_t nlab = b1[DMLC_AMD_LABEL] - b0[DMLC_AMD_LABEL];
       const uint64_t nw = b1[DMLC_AMD_WEIGHT] - b0[DMLC_AMD_WEIGHT];
       const uint64_t nq = b1[DMLC_AMD_QID] - b0[DMLC_AMD_QID];
+      const uint64_t nf = b1[DMLC_AMD_FIELD] - b0[DMLC_AMD_FIELD];
+      if (prm_.format == DMLC_AMD_LIBFM && nf != nidx)  // libfm_parser.h:127
+        throw dmlc::Error("Check failed: out->field.size() == out->index.size()");
       if (prm_.format == DMLC_AMD_CSV) {  // csv_parser.h:147-148
         if (nlab != 0 && nlab != rows)
           throw dmlc::Error("Check failed: out->label.size() == 0 || out->label.size() + 1 == out->offset.size()");
@@ -372,7 +380,7 @@ class HipParser : public dmlc::Parser<IndexType, DType> {
       blk.label = nlab ? reinterpret_cast<const DType *>(h_label_.p) + b0[DMLC_AMD_LABEL] : nullptr;
       blk.weight = nw ? h_weight_.p + b0[DMLC_AMD_WEIGHT] : nullptr;
       blk.qid = nq ? h_qid_.p + b0[DMLC_AMD_QID] : nullptr;
-      blk.field = nullptr;
+      blk.field = nf ? reinterpret_cast<const IndexType *>(h_field_.p) : nullptr;
       blk.index = reinterpret_cast<const IndexType *>(h_index_.p);
       blk.value = nval ? reinterpret_cast<const DType *>(h_value_.p) : nullptr;
       blocks_.push_back(blk);
@@ -405,10 +413,11 @@ class HipParser : public dmlc::Parser<IndexType, DType> {
   bool stop_ = false, ended_ = false;
   std::string error_;
   // device and pinned host buffers
-  DevBuf d_text_, d_cs_, d_res_, d_tab_, d_ws_, d_off_, d_label_, d_weight_, d_qid_, d_index_, d_value_;
+  DevBuf d_text_, d_cs_, d_res_, d_tab_, d_ws_, d_off_, d_label_, d_weight_, d_qid_, d_index_, d_field_,
+      d_value_;
   PinnedVec<uint64_t> h_off_, h_qid_, h_tab_;
   PinnedVec<float> h_weight_;
-  PinnedVec<char> h_label_, h_index_, h_value_;
+  PinnedVec<char> h_label_, h_index_, h_field_, h_value_;
   std::vector<dmlc::RowBlock<IndexType, DType>> blocks_;
   size_t cur_ = 0;
   size_t bytes_read_ = 0;
@@ -433,6 +442,7 @@ class HipRowIter : public dmlc::RowBlockIter<IndexType, DType> {
       if (b.weight) weight_.insert(weight_.end(), b.weight, b.weight + b.size);
       if (b.qid) qid_.insert(qid_.end(), b.qid, b.qid + b.size);
       index_.insert(index_.end(), b.index + lo, b.index + hi);
+      if (b.field) field_.insert(field_.end(), b.field + lo, b.field + hi);
       if (b.value) value_.insert(value_.end(), b.value + lo, b.value + hi);
       for (size_t j = lo; j < hi; ++j)
         if ((size_t)b.index[j] + 1 > num_col_) num_col_ = (size_t)b.index[j] + 1;
@@ -442,7 +452,7 @@ class HipRowIter : public dmlc::RowBlockIter<IndexType, DType> {
     block_.label = label_.empty() ? nullptr : label_.data();
     block_.weight = weight_.empty() ? nullptr : weight_.data();
     block_.qid = qid_.empty() ? nullptr : qid_.data();
-    block_.field = nullptr;
+    block_.field = field_.empty() ? nullptr : field_.data();
     block_.index = index_.empty() ? nullptr : index_.data();
     block_.value = value_.empty() ? nullptr : value_.data();
   }
@@ -460,7 +470,7 @@ class HipRowIter : public dmlc::RowBlockIter<IndexType, DType> {
   std::vector<DType> label_;
   std::vector<float> weight_;
   std::vector<uint64_t> qid_;
-  std::vector<IndexType> index_;
+  std::vector<IndexType> index_, field_;
   std::vector<DType> value_;
   size_t num_col_ = 0;
   bool at_start_ = true;

@@ -24,7 +24,7 @@ static int run(const char *uri, unsigned part, unsigned nparts, const char *type
   std::vector<uint64_t> offset(1, 0), qid;
   std::vector<D> label, value;
   std::vector<float> weight;
-  std::vector<I> index;
+  std::vector<I> index, field;
   size_t blocks = 0, bytes = 0, numcol = 0;
   auto push = [&](const dmlc::RowBlock<I, D> &b) {
     ++blocks;
@@ -34,6 +34,7 @@ static int run(const char *uri, unsigned part, unsigned nparts, const char *type
     if (b.weight) weight.insert(weight.end(), b.weight, b.weight + b.size);
     if (b.qid) qid.insert(qid.end(), b.qid, b.qid + b.size);
     index.insert(index.end(), b.index + b.offset[0], b.index + b.offset[b.size]);
+    if (b.field) field.insert(field.end(), b.field + b.offset[0], b.field + b.offset[b.size]);
     if (b.value) value.insert(value.end(), b.value + b.offset[0], b.value + b.offset[b.size]);
   };
   try {
@@ -69,6 +70,7 @@ static int run(const char *uri, unsigned part, unsigned nparts, const char *type
   dump(o + ".weight", weight);
   dump(o + ".qid", qid);
   dump(o + ".index", index);
+  dump(o + ".field", field);
   dump(o + ".value", value);
   std::vector<uint64_t> meta = {blocks, bytes, numcol};
   dump(o + ".meta", meta);

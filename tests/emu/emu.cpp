@@ -15,6 +15,7 @@
 #include "csv_core.h"
 #include "csv_fast.h"
 #include "dmlc_amd.h"
+#include "libfm_core.h"
 #include "libsvm_core.h"
 #include "svm_fast.h"
 
@@ -329,6 +330,44 @@ extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *c
         run_block([&](HostBlock &bk) { csv::tile<2>(a, *sh, bk, k); });
         delete sh;
       }
+  } else if (prm->format == DMLC_AMD_LIBFM) {  // mirrors launch_libfm (libfm.hip)
+    LibfmArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.text = text;
+    a.n = nbytes;
+    a.cs = cs;
+    a.nchunk = nchunks;
+    a.tile_bytes = T;
+    a.ntiles = (uint32_t)ntiles;
+    a.wide = prm->index_bits == 64;
+    a.indexing_mode = prm->indexing_mode;
+    a.tile_cnt = tile_cnt.data();
+    a.tile_base = tile_base.data();
+    a.offset = out->offset;
+    a.label = reinterpret_cast<float *>(out->label);
+    a.weight = out->weight;
+    a.index = out->index;
+    a.field = out->field;
+    a.value = reinterpret_cast<float *>(out->value);
+    for (int i = 0; i < 8; ++i) a.cap[i] = out->cap[i];
+    a.chunk_tab = chunk_table ? chunk_table : sink.data();
+    a.chunk_min = chunk_min.data();
+    a.err = err;
+    for (uint64_t k = 0; k < ntiles; ++k) {
+      svm::Shared *sh = new svm::Shared;
+      std::memset(sh, 0xCD, sizeof(*sh));
+      run_block([&](HostBlock &bk) { fm::tile<1>(a, *sh, bk, k); });
+      delete sh;
+    }
+    tile_scan(tile_cnt, tile_base, ntiles, res);
+    if (!count_only && out->offset && res[C_ROWS] < out->cap[C_ROWS] + 1) out->offset[res[C_ROWS]] = res[C_INDEX];
+    if (!count_only)
+      for (uint64_t k = 0; k < ntiles; ++k) {
+        svm::Shared *sh = new svm::Shared;
+        std::memset(sh, 0xCD, sizeof(*sh));
+        run_block([&](HostBlock &bk) { fm::tile<2>(a, *sh, bk, k); });
+        delete sh;
+      }
   } else {
     return DMLC_AMD_ERR_ARG;
   }
@@ -390,7 +429,7 @@ int main(int argc, char **argv) {
   const size_t vsz = prm.value_type == DMLC_AMD_I64 ? 8 : 4, isz = prm.index_bits == 64 ? 8 : 4;
   std::vector<uint64_t> offset(res[0] + 1);
   void *label = std::malloc(res[5] * vsz + 1), *value = std::malloc(res[2] * vsz + 1),
-       *index = std::malloc(res[1] * isz + 1);
+       *index = std::malloc(res[1] * isz + 1), *field = std::malloc(res[6] * isz + 1);
   std::vector<float> weight(res[3] + 1);
   std::vector<uint64_t> qid(res[4] + 1);
   std::vector<uint64_t> chunks((nch > 0 ? nch : 1) * 8, 0);
@@ -399,6 +438,7 @@ int main(int argc, char **argv) {
   csr.weight = weight.data();
   csr.qid = qid.data();
   csr.index = index;
+  csr.field = field;
   csr.value = value;
   uint64_t caps[8] = {res[0], res[1], res[2], res[3], res[4], res[5], res[6], 0};
   std::memcpy(csr.cap, caps, sizeof(caps));
@@ -411,11 +451,13 @@ int main(int argc, char **argv) {
   dump(o + ".weight", weight.data(), res2[3] * 4);
   dump(o + ".qid", qid.data(), res2[4] * 8);
   dump(o + ".index", index, res2[1] * isz);
+  dump(o + ".field", field, res2[6] * isz);
   dump(o + ".value", value, res2[2] * vsz);
   dump(o + ".chunks", chunks.data(), chunks.size() * 8);
   std::free(t);
   std::free(label);
   std::free(value);
   std::free(index);
+  std::free(field);
   return 0;
 }

@@ -52,7 +52,7 @@ def parse(data, chunk_offsets=None, fmt="libsvm", index_bits=32, value_type=0, i
             "label": np.fromfile(op + ".label", dtype=vt),
             "weight": np.fromfile(op + ".weight", dtype=np.float32),
             "qid": np.fromfile(op + ".qid", dtype=np.uint64),
-            "field": np.zeros(0, dtype=it),
+            "field": np.fromfile(op + ".field", dtype=it),
             "index": np.fromfile(op + ".index", dtype=it),
             "value": np.fromfile(op + ".value", dtype=vt),
             "chunk_table": np.fromfile(op + ".chunks", dtype=np.uint64).reshape(-1, 8),

@@ -122,3 +122,18 @@ def random_cuts(rng, data, nmax=8, anywhere=False):
     k = int(rng.integers(0, min(nmax, len(cand)) + 1)) if cand else 0
     cuts = sorted(set(rng.choice(cand, size=k, replace=False).tolist())) if k else []
     return [0] + cuts + [n]
+
+
+def libfm_rows(rng, rows, width, weights=False):
+    """Synthetic libfm text: 'label[:w] field:index:value ...' per line
+    (libfm_parser.h:67-144), ids 1-based and increasing, values %.9g."""
+    out = []
+    for _ in range(rows):
+        lab = "%d" % int(rng.integers(0, 2))
+        if weights:
+            lab += ":%.6g" % float(rng.random())
+        ids = np.cumsum(rng.integers(1, 9, size=width))
+        flds = rng.integers(1, 40, size=width)
+        vals = rng.random(width).astype(np.float32)
+        out.append(lab + " " + " ".join("%d:%d:%.9g" % (f, i, v) for f, i, v in zip(flds, ids, vals)))
+    return ("\n".join(out) + "\n").encode()

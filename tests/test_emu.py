@@ -12,7 +12,7 @@ from oracle import pyoracle as po
 from tests.emu import pyemu
 from tools import synth
 
-FMT = {po.LIBSVM: "libsvm", po.CSV: "csv"}
+FMT = {po.LIBSVM: "libsvm", po.CSV: "csv", po.LIBFM: "libfm"}
 
 
 def check_fail(h, fmt, offs):
@@ -50,14 +50,15 @@ def test_emu_goldens(case):
 
 def _fuzz(rng, fmt):
     alpha = {po.LIBSVM: list("0123456789") * 6 + list("  ::.-+eE#\tq") + ["qid:", "nan", "inf", "\r"],
-             po.CSV: list("0123456789") * 6 + list(",,,,.-+eE \t") + ["nan", "inf", "0x", "\xef\xbb\xbf"]}[fmt]
+             po.CSV: list("0123456789") * 6 + list(",,,,.-+eE \t") + ["nan", "inf", "0x", "\xef\xbb\xbf"],
+             po.LIBFM: list("0123456789") * 6 + list("  :::.-+eE#\t") + ["\r", "nan", "x"]}[fmt]
     lines = ["".join(alpha[int(i)] for i in rng.integers(0, len(alpha), int(rng.integers(0, 60))))
              for _ in range(int(rng.integers(1, 10)))]
     t = "\n".join(lines) + ("\n" if rng.random() < 0.5 else "")
     return t.encode("latin-1")
 
 
-@pytest.mark.parametrize("fmt", [po.LIBSVM, po.CSV])
+@pytest.mark.parametrize("fmt", [po.LIBSVM, po.CSV, po.LIBFM])
 def test_emu_fuzz_vs_oracle(fmt):
     rng = np.random.default_rng(99 + fmt)
     for it in range(60):
@@ -70,8 +71,10 @@ def test_emu_fuzz_vs_oracle(fmt):
             kw["tile_bytes"] = int(rng.integers(8, 64))
         if fmt == po.CSV and rng.random() < 0.3:
             kw["label_column"] = int(rng.integers(0, 3))
-        if fmt == po.LIBSVM and rng.random() < 0.3:
+        if fmt in (po.LIBSVM, po.LIBFM) and rng.random() < 0.3:
             kw["indexing_mode"] = int(rng.integers(-1, 2))
+        if fmt == po.LIBFM and rng.random() < 0.2:
+            kw["index_bits"] = 64
         okw = {k: v for k, v in kw.items() if k != "tile_bytes"}
         o = po.parse_chunks(data, offs, fmt=fmt, **okw)
         h = pyemu.parse(data, offs, FMT[fmt], **kw)

@@ -50,7 +50,7 @@ def gpu_parse(dm, data, chunk_offsets=None, fmt=po.LIBSVM, **kw):
     return h
 
 
-CASES = [c for c in load_cases() if c["params"]["fmt"] != po.LIBFM]
+CASES = load_cases()
 
 
 @pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
@@ -152,7 +152,8 @@ def test_gpu_long_lines_vs_oracle(dm):
 
 def _fuzz_text(rng, fmt):
     alpha = {po.LIBSVM: list("0123456789") * 6 + list("  ::.-+eE#\tq") + ["qid:", "nan", "inf", "\r"],
-             po.CSV: list("0123456789") * 6 + list(",,,,.-+eE \t") + ["nan", "inf", "0x", "\xef\xbb\xbf"]}[fmt]
+             po.CSV: list("0123456789") * 6 + list(",,,,.-+eE \t") + ["nan", "inf", "0x", "\xef\xbb\xbf"],
+             po.LIBFM: list("0123456789") * 6 + list("  :::.-+eE#\t") + ["\r", "nan", "x"]}[fmt]
     lines = []
     for _ in range(int(rng.integers(1, 12))):
         n = int(rng.integers(0, 60))
@@ -163,7 +164,7 @@ def _fuzz_text(rng, fmt):
     return t.encode("latin-1")
 
 
-@pytest.mark.parametrize("fmt", [po.LIBSVM, po.CSV])
+@pytest.mark.parametrize("fmt", [po.LIBSVM, po.CSV, po.LIBFM])
 def test_gpu_fuzz_vs_oracle(dm, fmt):
     rng = np.random.default_rng(4242 + fmt)
     for it in range(300):
@@ -191,7 +192,7 @@ def test_gpu_fuzz_vs_oracle(dm, fmt):
 
 
 def test_gpu_empty_and_tiny(dm):
-    for fmt in (po.LIBSVM, po.CSV):
+    for fmt in (po.LIBSVM, po.CSV, po.LIBFM):
         for d in (b"", b"\n", b"\r\n\r\n", b"1", b"1\n", b"   \n"):
             offs = [0, len(d)] if d else [0]
             _oracle_vs_gpu(dm, d, offs, fmt)
@@ -397,3 +398,15 @@ def test_gpu_fast_many_chunks_vs_oracle(dm, fmt):
                         - np.searchsorted(st, tl, "left")).max())
         h = _oracle_vs_gpu(dm, data, offs, fmt)
         assert h["path"] == ("exact" if per_tile > 32 else "fast"), (name, n_cuts, per_tile, h["path"])
+
+
+@pytest.mark.gpu
+def test_gpu_libfm_synthetic_vs_oracle(dm):
+    """libfm over many tiles and InputSplit-style chunks, 1-based ids with the
+    three indexing modes, 32- and 64-bit ids, weights on some rows."""
+    rng = np.random.default_rng(31337)
+    data = fuzz_text.libfm_rows(rng, 3000, 40) + fuzz_text.libfm_rows(rng, 200, 7, weights=True)
+    assert len(data) > 1 << 20
+    for kw in ({}, {"indexing_mode": 1}, {"indexing_mode": -1}, {"index_bits": 64, "tile_bytes": 4096}):
+        h = _oracle_vs_gpu(dm, data, _random_chunks(rng, data, 12), po.LIBFM, **kw)
+        assert h["path"] == "exact" and len(h["field"]) == len(h["index"]) > 100000

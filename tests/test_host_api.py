@@ -122,7 +122,7 @@ def run_api(tmp_path, uri, part=0, nparts=1, fmt="libsvm", index_bits=32, dtype=
     h = {"offset": np.fromfile(o + ".offset", np.uint64), "label": np.fromfile(o + ".label", vt),
          "weight": np.fromfile(o + ".weight", np.float32), "qid": np.fromfile(o + ".qid", np.uint64),
          "index": np.fromfile(o + ".index", it), "value": np.fromfile(o + ".value", vt),
-         "field": np.zeros(0, it), "meta": np.fromfile(o + ".meta", np.uint64)}
+         "field": np.fromfile(o + ".field", it), "meta": np.fromfile(o + ".meta", np.uint64)}
     return h
 
 
@@ -175,6 +175,27 @@ def test_api_synthetic_multifile_multipart(tmp_path, fmt):
             o, nch = oracle_files(contents, part, nparts, fmt=po.LIBSVM if fmt == "libsvm" else po.CSV)
             assert "error" not in h, (h, part, nparts, [len(c) for c in contents])
             assert diff(h, o) == [], (part, nparts)
+
+
+@pytest.mark.gpu
+def test_api_libfm_parser_and_rowiter(tmp_path):
+    """Parser<I,float>::Create(..., "libfm") (data.cc:206-209): fields ride with
+    the indices through the C++ API, both id widths, indexing_mode=-1."""
+    import fuzz_text
+    rng = np.random.default_rng(21)
+    # weights on every row (a chunk with weights on some rows only gives a
+    # RowBlock whose weight array is shorter than size, row_block.h:178-189)
+    contents = [fuzz_text.libfm_rows(rng, 500, 9, weights=True), fuzz_text.libfm_rows(rng, 300, 4, weights=True)]
+    d, _ = _write(tmp_path / "fm", contents)
+    for bits in (32, 64):
+        for uri, kw in ((d, {}), (d + "?indexing_mode=-1", {"indexing_mode": -1})):
+            h = run_api(tmp_path, uri, fmt="libfm", index_bits=bits)
+            o, _ = oracle_files(contents, fmt=po.LIBFM, index_bits=bits, **kw)
+            assert "error" not in h, h
+            assert len(h["field"]) == len(h["index"]) > 0 and diff(h, o) == [], (bits, uri)
+    hi = run_api(tmp_path, d, fmt="libfm", iter_=True)
+    o, _ = oracle_files(contents, fmt=po.LIBFM)
+    assert diff(hi, o) == []
 
 
 @pytest.mark.gpu
