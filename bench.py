@@ -38,12 +38,14 @@ CONFIGS = {
     "csv_1m_x256": ("csv", 1 << 20, 256, 2),
     "libsvm_1m_x2048": ("libsvm", 1 << 20, 2048, 3),
     "libsvm_32m_x64": ("libsvm", 32 << 20, 64, 4),
+    "libfm_1m_x64": ("libfm", 1 << 20, 64, None),  # SURVEY 8(f) row 3, not a BASELINE config
 }
 DESC = {
     "libsvm_1m_x128": "libsvm 1M rows x 128 nnz/row, device-resident",
     "csv_1m_x256": "CSV dense 1M rows x 256 float cols, device-resident",
     "libsvm_1m_x2048": "libsvm 1M rows x 2048 nnz/row, device-resident",
     "libsvm_32m_x64": "libsvm 32M rows x 64 nnz/row, chunks sharded across GPUs",
+    "libfm_1m_x64": "libfm 1M rows x 64 field:id:value/row, device-resident (exact kernels)",
 }
 
 
@@ -63,7 +65,7 @@ def cpu_baseline(text, starts, fmt, budget_s):
     """Reference CPU parser (oracle/_ref when it travelled here, else the C
     restatement) over a bounded prefix of this shard's chunks."""
     from oracle import pyoracle as po
-    f = po.LIBSVM if fmt == "libsvm" else po.CSV
+    f = {"libsvm": po.LIBSVM, "csv": po.CSV, "libfm": po.LIBFM}[fmt]
     nproc = os.cpu_count() or 1
     use_ref = po.ref_available()
     # the reference's thread cap: min(max(nprocs/2 - 4, 1), nthread=2), text_parser.h:33-34, data.cc:31
@@ -113,7 +115,7 @@ def main():
     if args.rows:
         rows = args.rows
     t0 = time.time()
-    text, _ = synth.rows(synth.LIBSVM if fmt == "libsvm" else synth.CSV, rows, width, seed=1,
+    text, _ = synth.rows({"libsvm": synth.LIBSVM, "csv": synth.CSV, "libfm": synth.LIBFM}[fmt], rows, width, seed=1,
                          row0=rank * rows)
     starts = dmlc_amd.text_chunk_starts(text)
     log("[rank %d] generated %s: %d rows, %.3f GB, %d chunks in %.1f s"

@@ -2,10 +2,13 @@
 #include "text_split.h"
 
 #include <dirent.h>
+#include <fcntl.h>
 #include <sys/stat.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <cstring>
+#include <thread>
 
 #include "dmlc/base.h"
 
@@ -79,7 +82,7 @@ TextSplit::TextSplit(const std::string &uri, unsigned part, unsigned nparts, siz
 }
 
 TextSplit::~TextSplit() {
-  if (fp_) fclose(fp_);
+  if (fd_ >= 0) close(fd_);
 }
 
 size_t TextSplit::FileOf(uint64_t off) const {
@@ -89,13 +92,51 @@ size_t TextSplit::FileOf(uint64_t off) const {
 }
 
 bool TextSplit::OpenAt(size_t file, uint64_t pos) {
-  if (fp_) fclose(fp_);
-  fp_ = nullptr;
+  if (fd_ >= 0) close(fd_);
+  fd_ = -1;
   if (file >= files_.size()) return false;
-  fp_ = fopen(files_[file].c_str(), "rb");
-  if (!fp_) throw dmlc::Error("Check failed: cannot open \"" + files_[file] + "\"");
-  if (fseeko(fp_, (off_t)pos, SEEK_SET) != 0) throw dmlc::Error("Check failed: seek in \"" + files_[file] + "\"");
+  fd_ = open(files_[file].c_str(), O_RDONLY);
+  if (fd_ < 0) throw dmlc::Error("Check failed: cannot open \"" + files_[file] + "\"");
+  file_pos_ = pos;
   return true;
+}
+
+// len bytes of the open file at pos (all present: the size was taken at
+// construction).  Large reads are split over threads: one core copies page
+// cache at a fraction of what the host's memory system moves.
+void TextSplit::ReadAt(char *buf, size_t len, uint64_t pos) {
+  auto span = [this](char *b, size_t n, uint64_t at) {
+    while (n) {
+      const ssize_t r = pread(fd_, b, n, (off_t)at);
+      if (r <= 0) throw dmlc::Error("Check failed: read of \"" + files_[file_ptr_] + "\"");
+      b += r;
+      n -= (size_t)r;
+      at += (uint64_t)r;
+    }
+  };
+  constexpr size_t kMinSplit = 2u << 20;
+  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  const size_t nt = std::min<size_t>(std::min<size_t>(4, hw), len / kMinSplit);
+  if (nt <= 1) {
+    span(buf, len, pos);
+    return;
+  }
+  const size_t per = (len + nt - 1) / nt;
+  std::vector<std::thread> th;
+  std::string err;
+  for (size_t i = 1; i < nt; ++i) {
+    const size_t o = i * per, n = std::min(per, len - o);
+    th.emplace_back([&, o, n] {
+      try {
+        span(buf + o, n, pos + o);
+      } catch (const std::exception &e) {
+        err = e.what();
+      }
+    });
+  }
+  span(buf, std::min(per, len), pos);
+  for (auto &t : th) t.join();
+  if (!err.empty()) throw dmlc::Error(err);
 }
 
 // Bytes from `pos` in `file` to the next record start: past the first newline
@@ -131,18 +172,20 @@ size_t TextSplit::Read(char *buf, size_t size) {
   if (offset_curr_ + size > offset_end_) size = offset_end_ - offset_curr_;
   if (size == 0) return 0;
   size_t left = size;
-  while (fp_) {
-    const size_t n = fread(buf, 1, left, fp_);
+  while (fd_ >= 0) {
+    const uint64_t remain = offset_[file_ptr_ + 1] - offset_[file_ptr_] - file_pos_;
+    const size_t n = (size_t)std::min<uint64_t>(left, remain);
+    if (n) ReadAt(buf, n, file_pos_);
     buf += n;
     left -= n;
+    file_pos_ += n;
     offset_curr_ += n;
     if (left == 0) break;
-    if (n == 0) {  // end of this file: newline, then the next file
-      *buf++ = '\n';
-      --left;
-      if (file_ptr_ + 1 >= files_.size()) break;
-      OpenAt(++file_ptr_, 0);
-    }
+    // end of this file: newline, then the next file
+    *buf++ = '\n';
+    --left;
+    if (file_ptr_ + 1 >= files_.size()) break;
+    OpenAt(++file_ptr_, 0);
   }
   return size - left;
 }
@@ -181,6 +224,55 @@ bool TextSplit::NextChunk(std::vector<char> *out) {
     overflow_.assign(buf.begin() + cut, buf.begin() + n);
     return true;
   }
+}
+
+TextSplit::Fill TextSplit::FillChunks(char *dst, size_t cap, size_t max_bytes, std::vector<uint64_t> *ends) {
+  size_t olen = overflow_.size();
+  if (olen > cap) return Fill{false, olen + 1};
+  std::memcpy(dst, overflow_.data(), olen);
+  size_t pos = 0;  // start of the current chunk in dst
+  Fill f{false, 0};
+  while (pos < max_bytes) {
+    size_t words = buffer_bytes_ / 4 + 1;  // as NextChunk: B, 2B+4, 4B+12, ...
+    bool cut_made = false;
+    for (;;) {
+      const size_t C = (words - 1) * 4;
+      if (C <= olen) {
+        words *= 2;
+        continue;
+      }
+      if (pos + C + 1 > cap) {  // the next chunk might not fit here
+        if (pos == 0) f.need = C + 1;
+        break;
+      }
+      size_t n = Read(dst + pos + olen, C - olen) + olen;
+      if (n == 0) {
+        f.end = true;
+        break;
+      }
+      if (n == olen) dst[pos + n++] = '\n';  // end of input mid-record
+      size_t cut = 0;
+      for (size_t p = n - 1; p > 0; --p) {
+        if (is_newline(dst[pos + p])) {
+          cut = p + 1;
+          break;
+        }
+      }
+      if (cut == 0) {  // no record boundary yet: read on with a bigger buffer
+        olen = n;
+        words *= 2;
+        continue;
+      }
+      pos += cut;
+      olen = n - cut;
+      ends->push_back(pos);
+      cut_made = true;
+      break;
+    }
+    if (!cut_made) break;
+  }
+  overflow_.assign(dst + pos, dst + pos + olen);
+  return f;
 }
 
 }  // namespace dmlc_amd

@@ -31,6 +31,17 @@ class TextSplit {
 
   // Appends the next chunk to *out; false at the end of the part.
   bool NextChunk(std::vector<char> *out);
+
+  // In-place form for the device pipeline: reads whole chunks straight into
+  // dst (capacity cap bytes) -- the same byte sequence and the same cuts as
+  // NextChunk -- until at least max_bytes are filled or the next chunk might
+  // not fit.  Each chunk's end offset (relative to dst) is appended to *ends.
+  // The partial record after the last cut is kept for the next call.
+  struct Fill {
+    bool end;     // the part is exhausted
+    size_t need;  // > 0: not even one chunk fits; call again with cap >= need
+  };
+  Fill FillChunks(char *dst, size_t cap, size_t max_bytes, std::vector<uint64_t> *ends);
   // Rewind to the start of the part.
   void BeforeFirst();
   // Bytes of this part's byte range consumed so far.
@@ -38,6 +49,7 @@ class TextSplit {
 
  private:
   size_t Read(char *buf, size_t size);
+  void ReadAt(char *buf, size_t len, uint64_t pos);  // pread, split over threads when large
   uint64_t SeekRecordBegin(size_t file, uint64_t pos);
   size_t FileOf(uint64_t off) const;
   bool OpenAt(size_t file, uint64_t pos);
@@ -46,7 +58,8 @@ class TextSplit {
   std::vector<uint64_t> offset_;  // files_.size() + 1 prefix sums of the sizes
   uint64_t offset_begin_ = 0, offset_end_ = 0, offset_curr_ = 0;
   size_t file_ptr_ = 0;
-  FILE *fp_ = nullptr;
+  int fd_ = -1;
+  uint64_t file_pos_ = 0;  // read position in files_[file_ptr_]
   size_t buffer_bytes_;
   std::vector<char> overflow_;  // partial record carried to the next chunk
 };

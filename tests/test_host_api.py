@@ -33,6 +33,9 @@ def _host():
                                       ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p),
                                       ctypes.POINTER(ctypes.c_uint64)]
     L.dmlc_amd_host_free.argtypes = [ctypes.c_void_p]
+    L.dmlc_amd_host_split_inplace.argtypes = [ctypes.c_char_p, ctypes.c_uint, ctypes.c_uint, ctypes.c_uint64,
+                                              ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p),
+                                              ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint64)]
     return L
 
 
@@ -41,6 +44,19 @@ def host_split(uri, part, nparts, buffer_bytes):
     buf, off, n = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_uint64()
     assert L.dmlc_amd_host_split(uri.encode(), part, nparts, buffer_bytes, ctypes.byref(buf),
                                  ctypes.byref(off), ctypes.byref(n)) == 0
+    offs = np.ctypeslib.as_array(ctypes.cast(off, ctypes.POINTER(ctypes.c_uint64)), (n.value + 1,)).copy()
+    data = ctypes.string_at(buf, int(offs[-1])) if offs[-1] else b""
+    L.dmlc_amd_host_free(buf)
+    L.dmlc_amd_host_free(off)
+    return [data[int(a):int(b)] for a, b in zip(offs[:-1], offs[1:])]
+
+
+def host_split_inplace(uri, part, nparts, buffer_bytes, batch_bytes, cap):
+    """The chunks through TextSplit::FillChunks (the device pipeline's reader)."""
+    L = _host()
+    buf, off, n = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_uint64()
+    assert L.dmlc_amd_host_split_inplace(uri.encode(), part, nparts, buffer_bytes, batch_bytes, cap,
+                                         ctypes.byref(buf), ctypes.byref(off), ctypes.byref(n)) == 0
     offs = np.ctypeslib.as_array(ctypes.cast(off, ctypes.POINTER(ctypes.c_uint64)), (n.value + 1,)).copy()
     data = ctypes.string_at(buf, int(offs[-1])) if offs[-1] else b""
     L.dmlc_amd_host_free(buf)
@@ -84,6 +100,10 @@ def test_host_split_matches_oracle(tmp_path):
             got = host_split(uri, part, nparts, buf)
             exp = po.split_text(contents, part, nparts, buffer_bytes=buf)
             assert got == exp, (it, part, nparts, buf)
+            # the in-place reader: same chunks, whatever the batch and buffer sizes
+            batch = int(rng.choice([1, 3 * buf, 1 << 20]))
+            cap = int(rng.choice([buf + 1, 2 * buf + 7, 4 << 20, 40 << 20]))
+            assert host_split_inplace(uri, part, nparts, buf, batch, cap) == exp, (it, part, nparts, buf, batch, cap)
         for p in paths:
             os.remove(p)
 

@@ -10,6 +10,8 @@
  *    uniform in [1,16]), value = fp32 uniform [0,1) from a 24-bit mantissa,
  *    printed "%.9g" (round-trips exactly).
  *  CSV row: C values uniform [-1,1) (24-bit mantissa), "%.9g", ',' separated.
+ *  libfm row: "<label>( <field>:<id>:<value>)*\n", the libsvm row's ids and
+ *    values with a field in [0,32) per feature (libfm_parser.h:67-144).
  */
 #include <stdint.h>
 #include <stdio.h>
@@ -44,6 +46,22 @@ static size_t fmt_libsvm_row(char *o, uint64_t seed, uint64_t r, int K) {
   return (size_t)(p - o);
 }
 
+static size_t fmt_libfm_row(char *o, uint64_t seed, uint64_t r, int K) {
+  uint64_t s = row_state(seed, r);
+  char *p = o;
+  *p++ = (char)('0' + (sm64(&s) & 1));
+  uint64_t id = 0;
+  for (int j = 0; j < K; ++j) {
+    uint64_t x = sm64(&s);
+    uint64_t gap = 1 + (x & 15);
+    id = j == 0 ? gap - 1 : id + gap;
+    float v = (float)(x >> 40) * (1.0f / 16777216.0f);
+    p += sprintf(p, " %u:%llu:%.9g", (unsigned)((x >> 4) & 31), (unsigned long long)id, (double)v);
+  }
+  *p++ = '\n';
+  return (size_t)(p - o);
+}
+
 static size_t fmt_csv_row(char *o, uint64_t seed, uint64_t r, int C) {
   uint64_t s = row_state(seed, r);
   char *p = o;
@@ -58,7 +76,8 @@ static size_t fmt_csv_row(char *o, uint64_t seed, uint64_t r, int C) {
 
 /* upper bound on the bytes of `nrows` rows */
 size_t synth_bound(int fmt, uint64_t nrows, int width) {
-  return fmt == 0 ? nrows * (size_t)(2 + width * 26) : nrows * (size_t)(width * 18 + 2);
+  return fmt == 0 ? nrows * (size_t)(2 + width * 26)
+                  : fmt == 2 ? nrows * (size_t)(2 + width * 30) : nrows * (size_t)(width * 18 + 2);
 }
 
 /* Format rows [row0, row0+nrows) into out (capacity cap); returns bytes, or 0
@@ -80,7 +99,8 @@ size_t synth_rows(int fmt, uint64_t row0, uint64_t nrows, int width, uint64_t se
     for (uint64_t r = r0; r < r1; ++r) {
       if (line_off) line_off[r] = n; /* block-relative; fixed below */
       n += fmt == 0 ? fmt_libsvm_row(buf + n, seed, row0 + r, width)
-                    : fmt_csv_row(buf + n, seed, row0 + r, width);
+                    : fmt == 2 ? fmt_libfm_row(buf + n, seed, row0 + r, width)
+                               : fmt_csv_row(buf + n, seed, row0 + r, width);
     }
     bbuf[b] = buf;
     bsz[b] = n;
