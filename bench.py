@@ -103,8 +103,13 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        ndev = torch.cuda.device_count()
+        if ndev >= world:  # one process per GPU: RCCL for the barriers and the max-over-ranks time
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:  # rehearsal with more ranks than GPUs (ranks share a card): gloo on the host
+            torch.cuda.set_device(local % ndev)
+            dist.init_process_group("gloo")
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -161,7 +166,8 @@ def main():
     elapsed = time.perf_counter() - t_start
     kern_ms, launches, kern_name = dmlc_amd.profile_end()
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64,
+                         device=dev if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     r = res.cpu().numpy().view(np.uint64)
