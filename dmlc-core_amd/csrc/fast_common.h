@@ -87,7 +87,7 @@ DA_HD void load16(const uint8_t *p, uint32_t w[4]) {
 }
 
 struct Nib {
-  uint32_t d, n, c, bad;
+  uint32_t d, n, c, bad, g;
 };
 DA_HD Nib classify_dword(uint32_t x) {  // 4-bit masks of 4 bytes; bad: a byte outside the grammar
   const uint32_t cls = classify4(x);
@@ -96,6 +96,7 @@ DA_HD Nib classify_dword(uint32_t x) {  // 4-bit masks of 4 bytes; bad: a byte o
   r.n = nib_n(cls);
   r.c = nib_c(cls);
   r.bad = ((cls + 0x7F7F7F7Fu) & 0x80808080u) != 0x80808080u || (x & 0x80808080u);
+  r.g = 0;
   return r;
 }
 
@@ -197,6 +198,7 @@ DA_HD Nib classify_dword_lut(uint32_t x, const uint32_t *cls) {
   r.n = (acc >> 16) & 0xFu;
   r.c = (acc >> 24) & 0xFu;
   r.bad = ((acc >> 8) & ~acc & 0xFu) != 0;
+  r.g = (acc >> 8) & 0xFu;
   return r;
 }
 
@@ -416,8 +418,8 @@ DA_HD uint32_t lead8(const uint32_t w[4], uint32_t s, uint32_t L) {
 // computed as a Markstein quotient (one multiply, two FMAs, tabulated
 // reciprocal).  *ok = false: exponent, long parts or a number that may
 // continue past the window (caller falls back to the byte decoder).
-DA_HD float wfloat32(const uint32_t w[4], const DecTables &tb, bool *ok) {
-  const uint32_t M = nd4(w[0]) | (nd4(w[1]) << 4) | (nd4(w[2]) << 8) | (nd4(w[3]) << 12);
+// M: bit i set when window byte i is not '0'..'9' (16 bits)
+DA_HD float wfloat32m(const uint32_t w[4], uint32_t M, const DecTables &tb, bool *ok) {
   const uint32_t b0 = w[0] & 0xFFu;
   const bool neg = b0 == '-';
   const uint32_t sg = (neg || b0 == '+') ? 1u : 0u;
@@ -449,16 +451,20 @@ DA_HD float wfloat32(const uint32_t w[4], const DecTables &tb, bool *ok) {
   *ok = true;
   return neg ? -value : value;
 }
+DA_HD float wfloat32(const uint32_t w[4], const DecTables &tb, bool *ok) {
+  return wfloat32m(w, nd4(w[0]) | (nd4(w[1]) << 4) | (nd4(w[2]) << 8) | (nd4(w[3]) << 12), tb, ok);
+}
 
 // ParseUnsignedInt (strtonum.h:392-428): [+] then up to 8 digits.  Returns
 // false on a leading '-' (the reference's fatal CHECK); *ok = false when the
 // digits may not fit the form (caller falls back).
-DA_HD bool wuint32(const uint32_t w[4], const DecTables &tb, uint64_t *out, bool *ok) {
+// M: bit i set when window byte i is not '0'..'9' (bits 0-11 used)
+DA_HD bool wuint32m(const uint32_t w[4], uint32_t M, const DecTables &tb, uint64_t *out, bool *ok) {
   const uint32_t b0 = w[0] & 0xFFu;
   *ok = true;
   if (b0 == '-') return false;
   const uint32_t s = b0 == '+' ? 1u : 0u;
-  const uint32_t M = nd4(w[0]) | (nd4(w[1]) << 4) | (nd4(w[2]) << 8) | 0x1000u;
+  M = (M & 0xFFFu) | 0x1000u;
   const uint32_t L = (uint32_t)ctz32(M & ~s) - s;
   if (L > 8u) {
     *ok = false;
@@ -467,6 +473,9 @@ DA_HD bool wuint32(const uint32_t w[4], const DecTables &tb, uint64_t *out, bool
   const uint32_t k = 8u - L;
   *out = (lead8(w, s, L) >> k) * tb.inv5[k];
   return true;
+}
+DA_HD bool wuint32(const uint32_t w[4], const DecTables &tb, uint64_t *out, bool *ok) {
+  return wuint32m(w, nd4(w[0]) | (nd4(w[1]) << 4) | (nd4(w[2]) << 8), tb, out, ok);
 }
 
 struct GSrc {  // text bytes; NUL at or beyond the chunk end (as Src), global memory

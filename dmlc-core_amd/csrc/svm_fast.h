@@ -41,6 +41,7 @@ struct Shared {  // LDS of one workgroup
   uint64_t md[kThreads + 1];  // slot 0: the segment before the tile; slot t+1: segment t
   uint64_t mn[kThreads + 1];
   uint64_t mc[kThreads + 1];
+  uint16_t g16[kThreads + 1];  // digit plane, bytes 0-15 of segment t (t = kThreads: the post-halo)
 };
 
 struct Tile {
@@ -279,8 +280,21 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
   // ---- classify: segment tid -> slot tid+1; lanes 0..15 also one word each
   // of the 64 bytes before the tile -> slot 0
   uint32_t bad = 0;
+  uint64_t G;  // digit plane of my segment: the decoders' digit masks come from it
   {
     const Masks m = classify64_lut(sh.c.text + kPre + tid * kSegB, sh.cls);
+    G = m.g;
+    sh.g16[tid] = (uint16_t)m.g;
+    if (tid == kWave) {  // digits of the 16 bytes after the tile (windows of my last runs)
+      uint32_t g = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        uint32_t x;
+        memcpy(&x, sh.c.text + kPre + kTile + 4 * i, 4);
+        g |= classify_dword_lut(x, sh.cls).g << (4 * i);
+      }
+      sh.g16[kThreads] = (uint16_t)g;
+    }
     sh.md[tid + 1] = m.d;
     sh.mn[tid + 1] = m.n;
     sh.mc[tid + 1] = m.c;
@@ -327,6 +341,12 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
   const bool one_chunk = sh.c.ncs == 0;  // no chunk boundary before cnext
   // the window decoders are exact when its 16 bytes belong to the run's chunk
   auto lim_of = [&](uint64_t q) { return one_chunk ? sh.c.cnext : t.next_cs(q); };
+  const uint64_t Gn = sh.g16[tid + 1];
+  // non-digit flags of the 16 window bytes at segment offset b (b < 64)
+  auto ndig16 = [&](uint32_t b) -> uint32_t {
+    const uint64_t x = (G >> b) | (b ? (Gn << (64u - b)) : 0ull);
+    return ~(uint32_t)x & 0xFFFFu;
+  };
   auto dec_float = [&](uint64_t q) -> float {
 #ifdef FSVM_ABL_NODEC  // timing ablation only (tools/build_variants.sh), never shipped
     return (float)(uint32_t)q;
@@ -337,7 +357,7 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
     if (q + 16 <= lim) {
       const W16 wq = win_at(sh.c.text, t.tlo, q);
       const uint32_t w4[4] = {(uint32_t)wq.lo, (uint32_t)(wq.lo >> 32), (uint32_t)wq.hi, (uint32_t)(wq.hi >> 32)};
-      v = wfloat32(w4, sh.dt, &ok);
+      v = wfloat32m(w4, ndig16((uint32_t)(q - P)), sh.dt, &ok);
     }
     if (!ok) v = slow_float(a.text, q, lim);
     return v;
@@ -352,7 +372,7 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
     if (q + 16 <= lim) {
       const W16 wq = win_at(sh.c.text, t.tlo, q);
       const uint32_t w4[4] = {(uint32_t)wq.lo, (uint32_t)(wq.lo >> 32), (uint32_t)wq.hi, (uint32_t)(wq.hi >> 32)};
-      pos = wuint32(w4, sh.dt, &v, &ok);
+      pos = wuint32m(w4, ndig16((uint32_t)(q - P)), sh.dt, &v, &ok);
     }
     if (!ok) pos = slow_uint(a.text, q, lim, a.wide, &v);
     if (!pos) {
