@@ -36,16 +36,17 @@ struct Shared {  // LDS of one workgroup
   uint64_t md[kThreads + 1];  // slot 0: the segment before the tile; slot t+1: segment t
   uint64_t mn[kThreads + 1];
   uint64_t ml[kThreads + 1];
-  uint32_t cls[256];  // byte classes: byte 0 number char, 1 outside the grammar, 2 newline, 3 delimiter
+  uint32_t cls[256];  // byte classes: byte 0 number char, 1 digit (without 0: outside the grammar), 2 newline, 3 delimiter
   DecTables dt;
+  uint16_t g16[kThreads + 1];  // digit plane, bytes 0-15 of segment t (t = kThreads: the post-halo)
   uint64_t segc;      // the tile's segmented carry (delimiters since the last row start before it)
 };
 
 DA_HD uint32_t class_of_csv(uint32_t b, uint32_t delim) {
   if (b == delim) return 0x01000000u;
-  if (is_digitchar(b)) return 0x00000001u;
+  if (is_digitchar(b)) return is_digit(b) ? 0x00000101u : 0x00000001u;
   if (b == '\n' || b == '\r') return 0x00010000u;
-  return 0x00000100u;
+  return 0x00000100u;  // outside the grammar: "digit" without "number char"
 }
 
 // segmented sum on 32 bits: bit 31 = "a row starts here", bits 0-30 the
@@ -178,15 +179,28 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
   // ---- classify: segment tid -> slot tid+1; lanes 0..15 also one dword
   // each of the 64 bytes before the tile -> slot 0
   uint32_t bad = 0;
+  uint64_t G;  // digit plane of my segment: the decoder's digit masks come from it
   {
     const Masks m = classify64_lut(sh.c.text + kPre + tid * kSegB, sh.cls);
+    G = m.g;
+    sh.g16[tid] = (uint16_t)m.g;
+    if (tid == kWave) {  // digits of the 16 bytes after the tile (windows of my last values)
+      uint32_t g = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        uint32_t x;
+        memcpy(&x, sh.c.text + kPre + kTile + 4 * i, 4);
+        g |= classify_dword_lut(x, sh.cls).g << (4 * i);
+      }
+      sh.g16[kThreads] = (uint16_t)g;
+    }
     sh.md[tid + 1] = m.d;
     sh.mn[tid + 1] = m.n;
     sh.ml[tid + 1] = m.c;
     // bytes past the end of the text are staged as blanks: judge valid bytes only
     const uint64_t P0 = t.tlo + (uint64_t)tid * kSegB;
     const uint64_t vmask = P0 >= a.n ? 0ull : (a.n - P0 >= 64 ? ~0ull : ((1ull << (a.n - P0)) - 1));
-    bad = (m.g & vmask) != 0;
+    bad = (m.g & ~m.d & vmask) != 0;
     if (tid < 16 && t.tlo > 0) {
       uint32_t x;
       memcpy(&x, sh.c.text + 4 * tid, 4);
@@ -243,14 +257,17 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
     if (sh.c.bad) atomic_or_u32(a.gate, 1u);
   }
   const bool one_chunk = sh.c.ncs == 0;
+  const uint64_t Gn = sh.g16[tid + 1];
   auto dec_float = [&](uint64_t q) -> float {
+    const uint32_t b = (uint32_t)(q - P);  // non-digit flags of the window from the digit plane
+    const uint32_t M = ~(uint32_t)((G >> b) | (b ? (Gn << (64u - b)) : 0ull)) & 0xFFFFu;
     const uint64_t lim = one_chunk ? sh.c.cnext : t.next_cs(q);
     bool ok = false;
     float v = 0.f;
     if (q + 16 <= lim) {
       const W16 wq = win_at(sh.c.text, t.tlo, q);
       const uint32_t w4[4] = {(uint32_t)wq.lo, (uint32_t)(wq.lo >> 32), (uint32_t)wq.hi, (uint32_t)(wq.hi >> 32)};
-      v = wfloat32(w4, sh.dt, &ok);
+      v = wfloat32m(w4, M, sh.dt, &ok);
     }
     if (!ok) {
       GSrc src{a.text, lim};
