@@ -61,6 +61,25 @@ def csr_bytes(counts, index_bits=32, vbytes=4):
             + vbytes * c[dmlc_amd.VALUE])
 
 
+def hbm_copy_rate(dev, nbytes=4 << 30, reps=5):
+    """Achievable HBM rate on this GPU for context: a device-to-device
+    copy of nbytes, (read + write bytes) / time, best of reps."""
+    import torch
+    a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    b = torch.empty_like(a)
+    b.copy_(a)
+    best = 1e30
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        b.copy_(a)
+        e1.record()
+        e1.synchronize()
+        best = min(best, e0.elapsed_time(e1) * 1e-3)
+    del a, b
+    return round(2 * nbytes / best / 1e9, 1)
+
+
 def cpu_baseline(text, starts, fmt, budget_s):
     """Reference CPU parser (oracle/_ref when it travelled here, else the C
     restatement) over a bounded prefix of this shard's chunks."""
@@ -215,6 +234,11 @@ def main():
                      "bytes_per_launch": dom_bytes, "avg_ms": round(dom_ms, 4)},
         "cpu_baseline": None,
     }
+    if rank == 0 and world == 1:
+        try:
+            line["hbm_copy"] = {"GBps": hbm_copy_rate(dev), "what": "torch device copy of 4 GiB, (read+write)/time"}
+        except Exception as e:  # context only, never fatal
+            line["hbm_copy"] = {"error": repr(e)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             line["cpu_baseline"] = cpu_baseline(text, starts, fmt, args.cpu_budget)
