@@ -110,6 +110,7 @@ def main():
     ap.add_argument("--config", default="libsvm_1m_x128", choices=sorted(CONFIGS))
     ap.add_argument("--rows", type=int, default=0, help="override rows per GPU")
     ap.add_argument("--tile-bytes", type=int, default=0)
+    ap.add_argument("--label-column", type=int, default=-1, help="csv: CSVParserParam::label_column")
     ap.add_argument("--cpu-budget", type=float, default=15.0,
                     help="seconds of CPU-baseline parsing (rank 0, N=1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -148,7 +149,8 @@ def main():
     d_text = torch.from_numpy(text).to(dev)
     d_starts = torch.from_numpy(starts).to(dev)
     nbytes = int(text.size)
-    p = dmlc_amd.DeviceParser(fmt, tile_bytes=args.tile_bytes)
+    pkw = {"label_column": args.label_column} if fmt == "csv" else {}
+    p = dmlc_amd.DeviceParser(fmt, tile_bytes=args.tile_bytes, **pkw)
     res = torch.zeros(16, dtype=torch.int64, device=dev)
     counts = p.count(d_text, d_starts, result=res)
     out = p.alloc(counts)
@@ -223,7 +225,8 @@ def main():
         "config": {"workload": DESC[args.config], "baseline_config": cfg_idx, "format": fmt,
                    "rows_per_gpu": rows, "width": width, "input_bytes_per_gpu": nbytes,
                    "csr_bytes_per_gpu": b_out, "nnz_per_gpu": int(counts[dmlc_amd.INDEX]),
-                   "chunks_per_gpu": len(starts) - 1, "parallelism": "shard%d" % world},
+                   "chunks_per_gpu": len(starts) - 1, "parallelism": "shard%d" % world,
+                   **({"label_column": args.label_column} if args.label_column >= 0 else {})},
         "hbm_frac_input": round(value / world / HBM_PEAK_GBS, 4),
         "hbm_frac_in_out": round((total_in + b_out * world) * args.steps / elapsed / 1e9
                                  / world / HBM_PEAK_GBS, 4),

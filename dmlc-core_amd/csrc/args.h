@@ -67,7 +67,10 @@ struct FastCsvArgs {
   int wide;
   uint32_t delim;
   int skip_if_gated;
+  int label_col;        // CSVParserParam::label_column, -1 = none
   uint64_t *offset;
+  float *label;         // one per row when label_col >= 0
+  uint64_t *labsum;     // [2], zeroed per launch: sum(labels - rows), sum(first delimiters - rows)
   void *index;
   float *value;
   uint64_t cap[8];

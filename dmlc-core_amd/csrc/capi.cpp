@@ -161,7 +161,9 @@ int dmlc_amd_parse(const void *d_text, uint64_t nbytes, const uint64_t *d_chunk_
   uint32_t *ctl = cv.take<uint32_t>(4);               // gate
   unsigned long long *ferr = cv.take<unsigned long long>(1);
   uint64_t *lb = cv.take<uint64_t>(nft * 8 + 1);
-  if (!tile_cnt || !tile_base || !chunk_min || !chunk_sink || !ctl || !ferr || !lb) return DMLC_AMD_ERR_ARG;
+  uint64_t *labsum = cv.take<uint64_t>(2);
+  if (!tile_cnt || !tile_base || !chunk_min || !chunk_sink || !ctl || !ferr || !lb || !labsum)
+    return DMLC_AMD_ERR_ARG;
   uint64_t *res = reinterpret_cast<uint64_t *>(d_result);
   const bool count_only = (prm->flags & DMLC_AMD_FLAG_COUNT_ONLY) != 0;
   const bool fill_only = (prm->flags & DMLC_AMD_FLAG_FILL_ONLY) != 0;
@@ -252,6 +254,9 @@ int dmlc_amd_parse(const void *d_text, uint64_t nbytes, const uint64_t *d_chunk_
     f.wide = a.wide;
     f.delim = a.delim;
     f.skip_if_gated = phase == dmlc_amd::kPhaseFill;
+    f.label_col = prm->label_column;
+    f.label = reinterpret_cast<float *>(out->label);
+    f.labsum = labsum;
     f.offset = a.offset;
     f.index = a.index;
     f.value = reinterpret_cast<float *>(a.value);
@@ -261,10 +266,10 @@ int dmlc_amd_parse(const void *d_text, uint64_t nbytes, const uint64_t *d_chunk_
     f.gate = ctl;
     f.err = ferr;
     f.res = res;
-    // the uniform-grammar CSV kernel: float values, no label / weight column,
-    // a delimiter the number decoder cannot consume (csv_fast.h)
-    const bool use_fast = nbytes > 0 && prm->value_type == DMLC_AMD_F32 && prm->label_column < 0 &&
-                          prm->weight_column < 0 && a.fast_delim && !(prm->flags & DMLC_AMD_FLAG_EXACT);
+    // the uniform-grammar CSV kernel: float values, no weight column, a
+    // delimiter the number decoder cannot consume (csv_fast.h)
+    const bool use_fast = nbytes > 0 && prm->value_type == DMLC_AMD_F32 && prm->weight_column < 0 &&
+                          a.fast_delim && !(prm->flags & DMLC_AMD_FLAG_EXACT);
     e = dmlc_amd::launch_csv(a, f, use_fast, res, phase, s);
   } else {  // DMLC_AMD_LIBFM
     dmlc_amd::LibfmArgs a;

@@ -37,6 +37,13 @@ __global__ void reopen_kernel(uint64_t *res, uint64_t *offset, uint64_t cap_rows
   if (offset && res[0] < cap_rows + 1) offset[res[0]] = res[1];
 }
 
+// label column: the single pass assumed one non-empty label field per row
+// (and, for column 0, a delimiter in every row); a nonzero check sum hands the
+// input to the exact kernels
+__global__ void label_check_kernel(const uint64_t *labsum, uint32_t *gate) {
+  if (labsum[0] != 0 || labsum[1] != 0) *gate |= 1u;
+}
+
 // the error of whichever path produced the result
 __global__ void select_kernel(uint64_t *res, const uint32_t *gate, const unsigned long long *ferr) {
   if (*gate == 0) res[8] = *ferr;
@@ -63,6 +70,7 @@ hipError_t launch_csv(const CsvArgs &a, const FastCsvArgs &f, bool use_fast, uin
   if (use_fast) {
     if ((e = hipMemsetAsync(f.err, 0xFF, sizeof(uint64_t), s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(f.lb, 0, (size_t)f.ntiles * 8 * sizeof(uint64_t), s)) != hipSuccess) return e;
+    if (f.label_col >= 0 && (e = hipMemsetAsync(f.labsum, 0, 2 * sizeof(uint64_t), s)) != hipSuccess) return e;
     if (phase == kPhaseCount) {
       prof_mark(0, s, "csv_fast_tile<1>");
       csv_fast_tile<1><<<f.ntiles, kThreads, 0, s>>>(f);
@@ -72,6 +80,7 @@ hipError_t launch_csv(const CsvArgs &a, const FastCsvArgs &f, bool use_fast, uin
       csv_fast_tile<2><<<f.ntiles, kThreads, 0, s>>>(f);
       prof_mark(1, s, "csv_fast_tile<2>");
     }
+    if (f.label_col >= 0) label_check_kernel<<<1, 1, 0, s>>>(f.labsum, gate);
   } else if ((e = hipMemsetAsync(f.err, 0xFF, sizeof(uint64_t), s)) != hipSuccess) {
     return e;
   }

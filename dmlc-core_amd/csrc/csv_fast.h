@@ -40,6 +40,7 @@ struct Shared {  // LDS of one workgroup
   DecTables dt;
   uint16_t g16[kThreads + 1];  // digit plane, bytes 0-15 of segment t (t = kThreads: the post-halo)
   uint64_t segc;      // the tile's segmented carry (delimiters since the last row start before it)
+  uint32_t nlab, nfirst;  // label_col >= 0: label tokens / first delimiters of rows in this tile
 };
 
 DA_HD uint32_t class_of_csv(uint32_t b, uint32_t delim) {
@@ -171,7 +172,10 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
   t.tlo = (uint64_t)k * kTile;
   t.thi = mn<uint64_t>(t.tlo + kTile, a.n);
   if (tid < kWave) chunk_list(a.cs, a.nchunk, t.tlo, t.thi, sh.c, bk);
-  if (tid == 0) sh.md[0] = sh.mn[0] = sh.ml[0] = 0;
+  if (tid == 0) {
+    sh.md[0] = sh.mn[0] = sh.ml[0] = 0;
+    sh.nlab = sh.nfirst = 0;
+  }
   sh.cls[tid] = class_of_csv((uint32_t)tid, a.delim);
   init_dec_tables(sh.dt, bk);
   stage(a.text, a.n, t.tlo, sh.c, bk);
@@ -297,21 +301,18 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
   if (tid < kWave) csv_look_back(a.lb, k, cnt4, a.gate, sh.c, bk, &sh.segc);
   bk.sync();
   const uint64_t bRows = sh.c.base[Q_ROWS], bVal = sh.c.base[Q_VALS], tcarry = sh.segc;
-  if (k + 1 == a.ntiles && tid == 0) {
-    const uint64_t rows = bRows + nR;
-    a.res[C_ROWS] = rows;
-    a.res[C_INDEX] = bVal + nT;
-    a.res[C_VALUE] = bVal + nT;
-    a.res[C_WEIGHT] = 0;
-    a.res[C_QID] = 0;
-    a.res[C_LABEL] = 0;
-    a.res[C_FIELD] = 0;
-    if (MODE == 2 && a.offset && rows < a.cap[C_ROWS] + 1) a.offset[rows] = bVal + nT;
-  }
-  if (MODE != 2) return;
-
-  // ---- stores: values and column indices, then row offsets
-  const uint64_t eR = bRows + (ex & 0xFFFF), eV = bVal + ((ex >> 16) & 0xFFFF);
+  // With a label column (csv_parser.h:111-112) the field at column label_col
+  // of every row is its label and the other fields keep their column minus one
+  // past it.  The single pass assumes every row holds exactly one non-empty
+  // label field (then labels = rows and a token's value rank is its token rank
+  // minus the labels before it) and checks that assumption: the tiles sum
+  // (label tokens - rows) and, for label_col 0 (where a row without a
+  // delimiter is the reference's fatal "Delimiter not found",
+  // csv_parser.h:128-132), (first delimiters - rows) into labsum; a nonzero
+  // sum sets the gate after this kernel and the exact kernels redo the input.
+  const bool has_lab = a.label_col >= 0;
+  const uint64_t Lc = has_lab ? (uint64_t)a.label_col : ~0ull;
+  const uint64_t eR = bRows + (ex & 0xFFFF), eT = bVal + ((ex >> 16) & 0xFFFF);
   const uint64_t sex = ex >> 32;  // segmented exclusive (flag in bit 31)
   const uint64_t carry = (sex >> 31) ? (sex & 0x7FFFFFFFull) : tcarry + (sex & 0x7FFFFFFFull);
   auto col_of = [&](uint32_t b) -> uint64_t {  // delimiters since the row start, token at bit b
@@ -320,37 +321,87 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
     if (r) return (uint64_t)popc64(L & below & (~0ull << (63 - clz64(r))));
     return carry + popc64(L & below);
   };
-  auto put = [&](uint64_t r, uint32_t b, float v) {
-    if (r < a.cap[C_VALUE] && r < a.cap[C_INDEX]) {
-      a.value[r] = v;
-      const uint64_t c = col_of(b);
-      if (a.wide) reinterpret_cast<uint64_t *>(a.index)[r] = c;
-      else reinterpret_cast<uint32_t *>(a.index)[r] = (uint32_t)c;
+  if (has_lab) {
+    uint32_t nl = 0, nf = 0;
+    if (Lc == 0) {
+      // column-0 labels are the row starts holding a token; a row's first
+      // delimiter is the first after its start (row starts are sparse)
+      nl = (uint32_t)popc64(RS & T);
+      const uint64_t fr = RS & (0ull - RS);
+      if (carry == 0 && (L & (fr ? fr - 1 : ~0ull))) nf = 1;  // the row carried in has none yet
+      for (uint64_t rs = RS; rs; rs &= rs - 1) {
+        const uint64_t r = rs & (0ull - rs), nx = (rs & (rs - 1)) & (0ull - (rs & (rs - 1)));
+        nf += (L & (nx ? nx - 1 : ~0ull) & ~(r | (r - 1))) != 0;
+      }
+    } else {
+      for (uint64_t m = T; m; m &= m - 1) nl += col_of((uint32_t)ctz64(m)) == Lc;
+    }
+    if (nl) atomic_add_u32(&sh.nlab, nl);
+    if (nf) atomic_add_u32(&sh.nfirst, nf);
+    bk.sync();
+    // only tiles whose rows straddle their ends add (a device-wide atomic per
+    // tile saturates near 88/us, MI355X_MICROARCH.md "dequeue")
+    if (tid == 0) {
+      if (sh.nlab != nR) atomic_add_u64(&a.labsum[0], (uint64_t)sh.nlab - (uint64_t)nR);
+      if (Lc == 0 && sh.nfirst != nR) atomic_add_u64(&a.labsum[1], (uint64_t)sh.nfirst - (uint64_t)nR);
+    }
+  }
+  if (k + 1 == a.ntiles && tid == 0) {
+    const uint64_t rows = bRows + nR, vals = bVal + nT - (has_lab ? rows : 0);
+    a.res[C_ROWS] = rows;
+    a.res[C_INDEX] = vals;
+    a.res[C_VALUE] = vals;
+    a.res[C_WEIGHT] = 0;
+    a.res[C_QID] = 0;
+    a.res[C_LABEL] = has_lab ? rows : 0;
+    a.res[C_FIELD] = 0;
+    if (MODE == 2 && a.offset && rows < a.cap[C_ROWS] + 1) a.offset[rows] = vals;
+  }
+  if (MODE != 2) return;
+
+  // ---- stores: values and column indices (labels), then row offsets
+  auto put = [&](uint64_t g, uint32_t b, float v) {  // g: global token rank
+    const uint64_t c = col_of(b);
+    if (has_lab) {
+      const uint64_t bit = 1ull << b;
+      const uint64_t row = eR + popc64(RS & ((bit - 1) | bit)) - 1;  // this token's row
+      if (c == Lc) {
+        if (row < a.cap[C_LABEL]) a.label[row] = v;
+        else raise_error(a.err, E_CAPACITY, P + b);
+        return;
+      }
+      g -= row + (c > Lc ? 1u : 0u);  // labels before this token
+    }
+    const uint64_t ci = c - (c > Lc ? 1u : 0u);
+    if (g < a.cap[C_VALUE] && g < a.cap[C_INDEX]) {
+      a.value[g] = v;
+      if (a.wide) reinterpret_cast<uint64_t *>(a.index)[g] = ci;
+      else reinterpret_cast<uint32_t *>(a.index)[g] = (uint32_t)ci;
     } else {
       raise_error(a.err, E_CAPACITY, P + b);
     }
   };
   {
     uint64_t m = T;
-    uint64_t r = eV;
+    uint64_t g = eT;
 #pragma unroll
     for (int u = 0; u < kB; ++u) {
       if (m) {
-        put(r, (uint32_t)ctz64(m), vb[u]);
+        put(g, (uint32_t)ctz64(m), vb[u]);
         m &= m - 1;
-        ++r;
+        ++g;
       }
     }
-    for (; m; m &= m - 1, ++r) {
+    for (; m; m &= m - 1, ++g) {
       const uint32_t b = (uint32_t)ctz64(m);
-      put(r, b, dec_float(P + b));
+      put(g, b, dec_float(P + b));
     }
   }
   {
     uint64_t r = eR;
     for (uint64_t m = RS; m; m &= m - 1, ++r) {
       const int b = ctz64(m);
-      if (r < a.cap[C_ROWS]) a.offset[r] = eV + popc64(T & ((1ull << b) - 1));
+      if (r < a.cap[C_ROWS]) a.offset[r] = eT + popc64(T & ((1ull << b) - 1)) - (has_lab ? r : 0);
       else raise_error(a.err, E_CAPACITY, P + b);
     }
   }
@@ -361,11 +412,12 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
       if (x < P || x >= P + kSegB || x >= t.thi) continue;
       const uint64_t below = (1ull << (x - P)) - 1;
       uint64_t *row = a.chunk_tab + (uint64_t)(sh.c.c_first + i) * 8;
-      row[C_ROWS] = eR + popc64(RS & below);
-      row[C_INDEX] = row[C_VALUE] = eV + popc64(T & below);
+      const uint64_t rows = eR + popc64(RS & below);
+      row[C_ROWS] = rows;
+      row[C_INDEX] = row[C_VALUE] = eT + popc64(T & below) - (has_lab ? rows : 0);
       row[C_WEIGHT] = 0;
       row[C_QID] = 0;
-      row[C_LABEL] = 0;
+      row[C_LABEL] = has_lab ? rows : 0;
       row[C_FIELD] = 0;
     }
   }

@@ -69,6 +69,14 @@ DA_HD uint32_t atomic_add_u32(uint32_t *p, uint32_t v) {  // returns the old val
 #endif
 }
 
+DA_HD void atomic_add_u64(uint64_t *p, uint64_t v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  atomicAdd((unsigned long long *)p, (unsigned long long)v);
+#else
+  __atomic_fetch_add(p, v, __ATOMIC_RELAXED);
+#endif
+}
+
 // Look-back words: one 8-byte {status, value} word per counter, stored and
 // polled whole by agent-scope relaxed atomics (sc1: no L1, no tearing), so no
 // fence or separate flag is needed (MI355X_MICROARCH.md, visibility: R2 form).

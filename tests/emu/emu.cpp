@@ -275,9 +275,10 @@ extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *c
     a.err = err;
     // mirrors launch_csv (csv.hip): uniform-grammar kernel first, exact tile
     // kernels when it sets the gate (or the parameters are outside its form)
-    const bool use_fast = nbytes > 0 && prm->value_type == DMLC_AMD_F32 && prm->label_column < 0 &&
-                          prm->weight_column < 0 && a.fast_delim && !(prm->flags & DMLC_AMD_FLAG_EXACT);
+    const bool use_fast = nbytes > 0 && prm->value_type == DMLC_AMD_F32 && prm->weight_column < 0 &&
+                          a.fast_delim && !(prm->flags & DMLC_AMD_FLAG_EXACT);
     uint32_t gate = use_fast ? 0u : 1u;
+    uint64_t labsum[2] = {0, 0};
     unsigned long long ferr = ~0ull;
     if (use_fast) {
       const uint64_t nft = (nbytes + fast::kTile - 1) / fast::kTile;
@@ -291,6 +292,9 @@ extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *c
       f.ntiles = (uint32_t)nft;
       f.wide = a.wide;
       f.delim = a.delim;
+      f.label_col = prm->label_column;
+      f.label = reinterpret_cast<float *>(out->label);
+      f.labsum = labsum;
       f.offset = out->offset;
       f.index = out->index;
       f.value = reinterpret_cast<float *>(out->value);
@@ -307,6 +311,7 @@ extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *c
         else run_block([&](HostBlock &bk) { fcsv::tile<2>(f, *sh, bk, (uint32_t)k); });
         delete sh;
       }
+      if (f.label_col >= 0 && (labsum[0] != 0 || labsum[1] != 0)) gate |= 1u;  // label_check_kernel
     }
     std::fprintf(stderr, "emu: csv path=%s\n", gate ? "exact" : "fast");
     if (!gate) {

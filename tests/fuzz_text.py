@@ -137,3 +137,28 @@ def libfm_rows(rng, rows, width, weights=False):
         vals = rng.random(width).astype(np.float32)
         out.append(lab + " " + " ".join("%d:%d:%.9g" % (f, i, v) for f, i, v in zip(flds, ids, vals)))
     return ("\n".join(out) + "\n").encode()
+
+
+def labeled_csv(rng, nlines, ncols, label_col, delim=",", defects=0.0):
+    """CSV with a label column: every row holds ncols non-empty numeric fields
+    (the single-pass kernel's label form) unless a defect is injected with
+    probability `defects`: an empty label field, a short row, a one-field row,
+    empty value fields or a trailing delimiter."""
+    out = []
+    for _ in range(nlines):
+        fields = ["%.9g" % v for v in (rng.random(ncols).astype(np.float32) * 2 - 1)]
+        fields[min(label_col, ncols - 1)] = str(int(rng.integers(0, 2)))
+        if rng.random() < defects:
+            kind = int(rng.integers(0, 5))
+            if kind == 0:
+                fields[min(label_col, ncols - 1)] = ""
+            elif kind == 1:
+                fields = fields[:int(rng.integers(1, max(2, label_col + 1)))]
+            elif kind == 2:
+                fields = fields[:1]
+            elif kind == 3:
+                fields[int(rng.integers(0, ncols))] = ""
+            else:
+                fields.append("")
+        out.append(delim.join(fields))
+    return ("\n".join(out) + "\n").encode()

@@ -205,3 +205,28 @@ def test_emu_fast_many_chunks():
             assert o["status"] == 0 and not check_fail(h, fmt, offs)
             assert diff(h, o) == [], (fmt, n_cuts, diff(h, o))
             assert h["path"] == ("exact" if cluster else "fast"), (fmt, n_cuts, h["path"])
+
+
+def test_emu_csv_fast_label_column():
+    """label_column on the single-pass CSV kernel: clean inputs stay on it;
+    empty labels, short rows, one-field rows (label 0: the reference's fatal
+    'Delimiter not found') go to the exact kernels -- the reference's result
+    (or error) either way."""
+    rng = np.random.default_rng(8080)
+    fast = 0
+    for it in range(24):
+        lc = int(rng.choice([0, 0, 1, 3]))
+        nl = 400 if it % 6 == 5 else int(rng.integers(1, 40))
+        data = fuzz_text.labeled_csv(rng, nl, int(rng.integers(lc + 2, lc + 12)), lc,
+                                     defects=0.0 if it % 2 == 0 else 0.1)
+        offs = fuzz_text.random_cuts(rng, data, 4)
+        o = po.parse_chunks(data, offs, fmt=po.CSV, label_column=lc)
+        h = pyemu.parse(data, offs, "csv", label_column=lc)
+        failed = check_fail(h, "csv", offs)
+        assert (o["status"] != 0) == failed, (it, lc, o["msg"], h["error"])
+        if not failed:
+            assert diff(h, o) == [], (it, lc, diff(h, o))
+        if it % 2 == 0:
+            assert h["path"] == "fast", it
+        fast += h["path"] == "fast"
+    assert fast >= 12

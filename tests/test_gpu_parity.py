@@ -410,3 +410,28 @@ def test_gpu_libfm_synthetic_vs_oracle(dm):
     for kw in ({}, {"indexing_mode": 1}, {"indexing_mode": -1}, {"index_bits": 64, "tile_bytes": 4096}):
         h = _oracle_vs_gpu(dm, data, _random_chunks(rng, data, 12), po.LIBFM, **kw)
         assert h["path"] == "exact" and len(h["field"]) == len(h["index"]) > 100000
+
+
+@pytest.mark.gpu
+def test_gpu_csv_fast_label_column_vs_oracle(dm):
+    """label_column on the single-pass CSV kernel (clean inputs of 2+ fields stay fast;
+    empty labels, short rows and one-field rows go exact with the reference's
+    result or error), plus canonical synthetic CSV with label_column 0 and 5."""
+    rng = np.random.default_rng(9090)
+    fast = 0
+    for it in range(60):
+        lc = int(rng.choice([0, 0, 1, 3]))
+        nl = 3000 if it % 10 == 9 else int(rng.integers(1, 60))
+        data = fuzz_text.labeled_csv(rng, nl, int(rng.integers(lc + 2, lc + 20)), lc,
+                                     defects=0.0 if it % 2 == 0 else 0.08)
+        offs = fuzz_text.random_cuts(rng, data, 6)
+        h = _oracle_vs_gpu(dm, data, offs, po.CSV, label_column=lc)
+        if it % 2 == 0:
+            assert h["path"] == "fast", it
+        fast += h["path"] == "fast"
+    assert fast >= 30
+    text, _ = synth.rows(synth.CSV, 6000, 256, seed=17)
+    offs = dm.text_chunk_starts(text, 1 << 20).tolist()
+    for lc in (0, 5):
+        h = _oracle_vs_gpu(dm, text.tobytes(), offs, po.CSV, label_column=lc)
+        assert h["path"] == "fast" and len(h["label"]) == 6000 and len(h["index"]) == 6000 * 255
