@@ -7,6 +7,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 
@@ -114,9 +115,13 @@ void TextSplit::ReadAt(char *buf, size_t len, uint64_t pos) {
       at += (uint64_t)r;
     }
   };
-  constexpr size_t kMinSplit = 2u << 20;
-  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-  const size_t nt = std::min<size_t>(std::min<size_t>(4, hw), len / kMinSplit);
+  constexpr size_t kMinSplit = 1u << 20;
+  static const size_t kThreadsMax = [] {
+    const char *e = std::getenv("DMLC_AMD_READ_THREADS");
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    return (size_t)std::min<unsigned>(e ? std::max(1, std::atoi(e)) : 4u, hw);
+  }();
+  const size_t nt = std::min<size_t>(kThreadsMax, len / kMinSplit);
   if (nt <= 1) {
     span(buf, len, pos);
     return;
