@@ -58,6 +58,7 @@ struct FastSvmArgs {
 };
 
 // Single-pass uniform-grammar CSV kernel (csv_fast.h).
+constexpr int kLabShards = 64;  // FastCsvArgs::labsum shards, one 64-byte line each
 struct FastCsvArgs {
   const uint8_t *text;
   uint64_t n;
@@ -70,7 +71,8 @@ struct FastCsvArgs {
   int label_col;        // CSVParserParam::label_column, -1 = none
   uint64_t *offset;
   float *label;         // one per row when label_col >= 0
-  uint64_t *labsum;     // [2], zeroed per launch: sum(labels - rows), sum(first delimiters - rows)
+  uint64_t *labsum;     // [kLabShards][8], zeroed per launch: words 0/1 = sum(labels - rows),
+                        // sum(first delimiters - rows), sharded by tile (csv_fast.h)
   void *index;
   float *value;
   uint64_t cap[8];

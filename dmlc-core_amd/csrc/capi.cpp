@@ -130,7 +130,8 @@ size_t dmlc_amd_workspace_bytes(uint64_t nbytes, int nchunks, const dmlc_amd_par
   const uint64_t ntiles = (nbytes + T - 1) / T;
   const uint64_t nc = nchunks > 0 ? (uint64_t)nchunks : 1;
   const uint64_t nft = (nbytes + kFastTile - 1) / kFastTile;
-  return (size_t)((2 * ntiles * kSlots + nc + nc * 8 + nft * 8) * sizeof(uint64_t) + 11 * 256);
+  return (size_t)((2 * ntiles * kSlots + nc + nc * 8 + nft * 8 + dmlc_amd::kLabShards * 8) * sizeof(uint64_t) +
+                  11 * 256);
 }
 
 int dmlc_amd_parse(const void *d_text, uint64_t nbytes, const uint64_t *d_chunk_starts, int nchunks,
@@ -161,7 +162,7 @@ int dmlc_amd_parse(const void *d_text, uint64_t nbytes, const uint64_t *d_chunk_
   uint32_t *ctl = cv.take<uint32_t>(4);               // gate
   unsigned long long *ferr = cv.take<unsigned long long>(1);
   uint64_t *lb = cv.take<uint64_t>(nft * 8 + 1);
-  uint64_t *labsum = cv.take<uint64_t>(2);
+  uint64_t *labsum = cv.take<uint64_t>(dmlc_amd::kLabShards * 8);
   if (!tile_cnt || !tile_base || !chunk_min || !chunk_sink || !ctl || !ferr || !lb || !labsum)
     return DMLC_AMD_ERR_ARG;
   uint64_t *res = reinterpret_cast<uint64_t *>(d_result);

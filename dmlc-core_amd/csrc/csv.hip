@@ -41,7 +41,14 @@ __global__ void reopen_kernel(uint64_t *res, uint64_t *offset, uint64_t cap_rows
 // (and, for column 0, a delimiter in every row); a nonzero check sum hands the
 // input to the exact kernels
 __global__ void label_check_kernel(const uint64_t *labsum, uint32_t *gate) {
-  if (labsum[0] != 0 || labsum[1] != 0) *gate |= 1u;
+  const uint32_t i = threadIdx.x;  // kLabShards threads, one wave
+  const uint64_t s0 = labsum[i * 8], s1 = labsum[i * 8 + 1];
+  uint64_t a = s0, b = s1;
+  for (int d = 32; d >= 1; d >>= 1) {
+    a += __shfl_xor(a, d, kWave);
+    b += __shfl_xor(b, d, kWave);
+  }
+  if (i == 0 && (a != 0 || b != 0)) *gate |= 1u;
 }
 
 // the error of whichever path produced the result
@@ -70,7 +77,9 @@ hipError_t launch_csv(const CsvArgs &a, const FastCsvArgs &f, bool use_fast, uin
   if (use_fast) {
     if ((e = hipMemsetAsync(f.err, 0xFF, sizeof(uint64_t), s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(f.lb, 0, (size_t)f.ntiles * 8 * sizeof(uint64_t), s)) != hipSuccess) return e;
-    if (f.label_col >= 0 && (e = hipMemsetAsync(f.labsum, 0, 2 * sizeof(uint64_t), s)) != hipSuccess) return e;
+    if (f.label_col >= 0 &&
+        (e = hipMemsetAsync(f.labsum, 0, kLabShards * 8 * sizeof(uint64_t), s)) != hipSuccess)
+      return e;
     if (phase == kPhaseCount) {
       prof_mark(0, s, "csv_fast_tile<1>");
       csv_fast_tile<1><<<f.ntiles, kThreads, 0, s>>>(f);
@@ -80,7 +89,7 @@ hipError_t launch_csv(const CsvArgs &a, const FastCsvArgs &f, bool use_fast, uin
       csv_fast_tile<2><<<f.ntiles, kThreads, 0, s>>>(f);
       prof_mark(1, s, "csv_fast_tile<2>");
     }
-    if (f.label_col >= 0) label_check_kernel<<<1, 1, 0, s>>>(f.labsum, gate);
+    if (f.label_col >= 0) label_check_kernel<<<1, kLabShards, 0, s>>>(f.labsum, gate);
   } else if ((e = hipMemsetAsync(f.err, 0xFF, sizeof(uint64_t), s)) != hipSuccess) {
     return e;
   }

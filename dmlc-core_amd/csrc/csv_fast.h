@@ -339,11 +339,13 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
     if (nl) atomic_add_u32(&sh.nlab, nl);
     if (nf) atomic_add_u32(&sh.nfirst, nf);
     bk.sync();
-    // only tiles whose rows straddle their ends add (a device-wide atomic per
-    // tile saturates near 88/us, MI355X_MICROARCH.md "dequeue")
+    // only tiles whose rows straddle their ends add, into one of kLabShards
+    // lines (one device-wide counter saturates near 88 atomics/us,
+    // MI355X_MICROARCH.md "dequeue")
     if (tid == 0) {
-      if (sh.nlab != nR) atomic_add_u64(&a.labsum[0], (uint64_t)sh.nlab - (uint64_t)nR);
-      if (Lc == 0 && sh.nfirst != nR) atomic_add_u64(&a.labsum[1], (uint64_t)sh.nfirst - (uint64_t)nR);
+      uint64_t *sum = a.labsum + (uint64_t)(k % kLabShards) * 8;
+      if (sh.nlab != nR) atomic_add_u64(&sum[0], (uint64_t)sh.nlab - (uint64_t)nR);
+      if (Lc == 0 && sh.nfirst != nR) atomic_add_u64(&sum[1], (uint64_t)sh.nfirst - (uint64_t)nR);
     }
   }
   if (k + 1 == a.ntiles && tid == 0) {

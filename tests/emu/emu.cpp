@@ -278,7 +278,8 @@ extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *c
     const bool use_fast = nbytes > 0 && prm->value_type == DMLC_AMD_F32 && prm->weight_column < 0 &&
                           a.fast_delim && !(prm->flags & DMLC_AMD_FLAG_EXACT);
     uint32_t gate = use_fast ? 0u : 1u;
-    uint64_t labsum[2] = {0, 0};
+    std::vector<uint64_t> labsum_v(kLabShards * 8, 0);
+    uint64_t *labsum = labsum_v.data();
     unsigned long long ferr = ~0ull;
     if (use_fast) {
       const uint64_t nft = (nbytes + fast::kTile - 1) / fast::kTile;
@@ -311,7 +312,14 @@ extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *c
         else run_block([&](HostBlock &bk) { fcsv::tile<2>(f, *sh, bk, (uint32_t)k); });
         delete sh;
       }
-      if (f.label_col >= 0 && (labsum[0] != 0 || labsum[1] != 0)) gate |= 1u;  // label_check_kernel
+      if (f.label_col >= 0) {  // label_check_kernel
+        uint64_t s0 = 0, s1 = 0;
+        for (int i = 0; i < kLabShards; ++i) {
+          s0 += labsum[i * 8];
+          s1 += labsum[i * 8 + 1];
+        }
+        if (s0 != 0 || s1 != 0) gate |= 1u;
+      }
     }
     std::fprintf(stderr, "emu: csv path=%s\n", gate ? "exact" : "fast");
     if (!gate) {
