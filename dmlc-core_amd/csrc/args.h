@@ -48,6 +48,7 @@ struct FastSvmArgs {
   float *label;
   float *weight;
   void *index;
+  void *field;          // libfm: one field id per index (IndexType); null for libsvm
   float *value;
   uint64_t cap[8];
   uint64_t *chunk_tab;  // may be null

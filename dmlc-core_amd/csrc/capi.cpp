@@ -295,7 +295,31 @@ int dmlc_amd_parse(const void *d_text, uint64_t nbytes, const uint64_t *d_chunk_
     a.chunk_tab = d_chunk_table ? d_chunk_table : chunk_sink;
     a.chunk_min = chunk_min;
     a.err = reinterpret_cast<unsigned long long *>(res + 8);
-    e = dmlc_amd::launch_libfm(a, res, phase, s);
+    a.gate = ctl;
+    dmlc_amd::FastSvmArgs f;  // the single-pass kernel with the libfm roles (svm_fast.h)
+    std::memset(&f, 0, sizeof(f));
+    f.text = a.text;
+    f.n = nbytes;
+    f.cs = d_chunk_starts;
+    f.nchunk = nchunks;
+    f.ntiles = (uint32_t)nft;
+    f.wide = a.wide;
+    f.indexing_mode = prm->indexing_mode;
+    f.skip_if_gated = phase == dmlc_amd::kPhaseFill;
+    f.offset = a.offset;
+    f.label = a.label;
+    f.weight = a.weight;
+    f.index = a.index;
+    f.field = a.field;
+    f.value = a.value;
+    for (int i = 0; i < 8; ++i) f.cap[i] = out->cap[i];
+    f.chunk_tab = d_chunk_table;
+    f.lb = lb;
+    f.gate = ctl;
+    f.err = ferr;
+    f.res = res;
+    const bool use_fast = nbytes > 0 && prm->indexing_mode >= 0 && !(prm->flags & DMLC_AMD_FLAG_EXACT);
+    e = dmlc_amd::launch_libfm(a, f, use_fast, res, phase, s);
   }
   g_last_hip = e;
   return e == hipSuccess ? DMLC_AMD_OK : DMLC_AMD_ERR_HIP;

@@ -23,7 +23,8 @@ void prof_mark(int end, hipStream_t s, const char *kernel);
 // kernels (a) run when it sets the gate word (f.gate), or always when !use_fast.
 hipError_t launch_libsvm(const LibsvmArgs &a, const FastSvmArgs &f, bool use_fast, uint64_t *res,
                          int phase, hipStream_t s);
-hipError_t launch_libfm(const LibfmArgs &a, uint64_t *res, int phase, hipStream_t s);
+hipError_t launch_libfm(const LibfmArgs &a, const FastSvmArgs &f, bool use_fast, uint64_t *res, int phase,
+                        hipStream_t s);
 hipError_t launch_csv(const CsvArgs &a, const FastCsvArgs &f, bool use_fast, uint64_t *res, int phase,
                       hipStream_t s);
 

@@ -224,6 +224,7 @@ DA_HDF void walk(const LibfmArgs &a, Src &src, const uint32_t *r1bits, uint64_t 
 // The tile body.  MODE 1 = count pass, MODE 2 = write pass.
 template <int MODE, class BK>
 DA_HDF void tile(const LibfmArgs &a, svm::Shared &sh, BK &bk, uint64_t k) {
+  if (a.gate && *a.gate == 0) return;  // the uniform-grammar kernel handled this input
   const uint64_t tlo = k * a.tile_bytes;
   if (tlo >= a.n) return;
   const uint64_t thi = mn(tlo + a.tile_bytes, a.n);

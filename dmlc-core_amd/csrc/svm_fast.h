@@ -226,6 +226,120 @@ DA_HD SegOut segment_roles(const Tile &t, int tid) {
   return o;
 }
 
+// ---- libfm (LibFMParser::ParseBlock, libfm_parser.h:67-144) in the same
+// uniform grammar.  A line is label[:weight] then ParseTriple groups
+// field:index[:value] (strtonum.h:718-772).  With K = runs whose gap holds ':'
+// and F = the other non-label runs (fields, v1), the roles are
+//   W = K after a label, I = K after a field, V = K after an index;
+// a K run after a value or weight ("f:i:v:x", "l:w:x") re-pairs in the
+// reference and leaves the fast path, as does a dangling ':' at a line end.
+// A field is stored only when its index follows (r >= 2); every field is
+// still checked for a '-' sign (the reference decodes every v1).
+enum : uint32_t { RF_NONE = 0, RF_L = 1, RF_W = 2, RF_F = 3, RF_I = 4, RF_V = 5, RF_BAD = 6 };
+
+// role of the run starting at q (chunk start f <= q): walks back through
+// the ':'-joined chain to its label or field (at most three runs)
+DA_HD uint32_t fm_role_of(const Tile &t, uint64_t q, uint64_t f) {
+  uint32_t nk = 0;  // ':' gaps walked over
+  for (;;) {
+    uint32_t base;
+    if (q == f) {
+      base = RF_L;
+    } else {
+      const uint64_t p = t.last_bit(0, f, q);
+      if (p == kNone || t.last_bit(2, p + 1, q) != kNone) {
+        base = RF_L;
+      } else if (t.last_bit(3, p + 1, q) == kNone) {
+        base = RF_F;
+      } else {
+        if (++nk > 2) return RF_BAD;
+        const uint64_t x = t.last_bit(1, f, p);
+        q = x == kNone ? f : x + 1;
+        continue;
+      }
+    }
+    if (nk == 0) return base;
+    if (base == RF_L) return nk == 1 ? RF_W : RF_BAD;
+    return nk == 1 ? RF_I : RF_V;
+  }
+}
+
+struct SegOutFm {
+  uint64_t L, W, I, V, F;
+  uint32_t bad;
+};
+
+// previous-run propagation: bit x of the result = the run before run start x
+// has its start bit in X (cin: the run before the segment does)
+DA_HD uint64_t prev_of(uint64_t RS, uint64_t X, uint32_t cin) {
+  const uint64_t Z = ~RS, xs = X << 1;
+  return ((Z + (xs & Z) + cin) | xs) & RS;
+}
+
+DA_HD SegOutFm segment_roles_fm(const Tile &t, int tid) {
+  SegOutFm o;
+  o.L = o.W = o.I = o.V = o.F = 0;
+  o.bad = 0;
+  const FastSvmArgs &a = *t.a;
+  const uint64_t P = t.tlo + (uint64_t)tid * kSegB;
+  if (P >= a.n) return o;
+  const int nv = (int)mn<uint64_t>(64, a.n - P);
+  const uint64_t valid = nv == 64 ? ~0ull : ((1ull << nv) - 1);
+  const uint64_t D = t.sh->md[tid + 1], N = t.sh->mn[tid + 1], C = t.sh->mc[tid + 1];
+  uint64_t S = 0;
+  for (uint32_t i = 0; i < t.sh->c.ncs; ++i) {
+    const uint64_t x = t.sh->c.csl[i];
+    if (x >= P && x < P + (uint64_t)nv) S |= 1ull << (x - P);
+  }
+  // ---- carry-in (the general look-back over the LDS masks)
+  uint32_t dc = 0, ginl = 0, ginc = 0, prole = RF_NONE;
+  const uint64_t F = t.floor_of(P);
+  if (P != F) {
+    uint64_t d, n, c;
+    t.seg((P - 1) >> 6, &d, &n, &c);
+    dc = (uint32_t)(d >> 63) & 1u;
+    if (dc) {
+      const uint64_t x = t.last_bit(1, F, P);
+      prole = fm_role_of(t, x == kNone ? F : x + 1, F);
+    } else {
+      const uint64_t p = t.last_bit(0, F, P);
+      if (p == kNone) {
+        ginl = 1;
+      } else {
+        const uint64_t ln = t.last_bit(2, p + 1, P);
+        ginl = ln != kNone;
+        ginc = t.last_bit(3, ginl ? ln + 1 : p + 1, P) != kNone;
+        const uint64_t x = t.last_bit(1, F, p);
+        prole = fm_role_of(t, x == kNone ? F : x + 1, F);
+      }
+    }
+  }
+  if (prole == RF_BAD) o.bad = 1;
+  // ---- roles inside the segment
+  const uint64_t RS = (D & ~((D << 1) | dc)) | (D & S);
+  const uint64_t G = ~D & valid;
+  const uint64_t NS = N | S;
+  uint32_t co;
+  const uint64_t t1 = add_carry(G, NS & G, ginl, &co);
+  const uint64_t L = RS & (t1 | S);
+  const uint64_t G2 = G & ~NS;
+  const uint64_t t2 = add_carry(G2, C & G2, ginc, &co);
+  if (t2 & (NS | ~valid)) o.bad = 1;  // "x:" at a line end: ParseTriple decodes past it
+  if (co && (P + 64 >= a.n || t.is_cs(P + 64))) o.bad = 1;
+  const uint64_t K = RS & t2 & ~L;
+  const uint64_t Fr = RS & ~L & ~K;
+  const uint64_t W = K & prev_of(RS, L, prole == RF_L);
+  const uint64_t I = K & prev_of(RS, Fr, prole == RF_F);
+  const uint64_t V = K & prev_of(RS, I, prole == RF_I);
+  if (K & ~(W | I | V)) o.bad = 1;
+  o.L = L;
+  o.W = W;
+  o.I = I;
+  o.V = V;
+  o.F = Fr;
+  return o;
+}
+
 // The exact byte decoders: rare on this path (exponents, runs that may cross
 // the 16-byte window or a chunk end, 9+ digit indices).
 // (Measured: out of line they cost more than the code size saves, so they
@@ -248,7 +362,7 @@ FSVM_COLD bool slow_uint(const uint8_t *text, uint64_t q, uint64_t lim, int wide
 }
 
 // MODE 1: count only (size query); MODE 2: parse and write.
-template <int MODE, class BK>
+template <int MODE, bool FM = false, class BK>
 DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
   // Tile k = workgroup k (its blockIdx).  The look-back needs every tile's
   // predecessors to become resident eventually; workgroups are dispatched in
@@ -316,7 +430,19 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
   return;
 #endif
   // ---- roles, counts, eligibility
-  const SegOut so = segment_roles(t, tid);
+  SegOut so;
+  uint64_t soF = 0;  // libfm: every field run (v1), for the sign check
+  if constexpr (FM) {
+    const SegOutFm sf = segment_roles_fm(t, tid);
+    so.L = sf.L;
+    so.W = sf.W;
+    so.I = sf.I;
+    so.V = sf.V;
+    so.bad = sf.bad;
+    soF = sf.F;
+  } else {
+    so = segment_roles(t, tid);
+  }
   if (so.bad | bad) atomic_or_u32(&sh.c.bad, 1u);
   // per-thread role counts packed in 16-bit fields (a tile holds < 2^16 runs)
   const uint64_t mine = (uint64_t)popc64(so.L) | ((uint64_t)popc64(so.W) << 16) |
@@ -443,7 +569,7 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
     a.res[C_WEIGHT] = bW + nW;
     a.res[C_QID] = 0;
     a.res[C_LABEL] = rows;
-    a.res[C_FIELD] = 0;
+    a.res[C_FIELD] = FM ? bIdx + nI : 0;
     if (MODE == 2 && a.offset && rows < a.cap[C_ROWS] + 1) a.offset[rows] = bIdx + nI;
   }
   if (MODE != 2) return;
@@ -507,6 +633,40 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
       put_float(bpos, dec_float(P + bpos));
     }
   }
+  if constexpr (FM) {
+    // every v1 is decoded by the reference: a '-' field is the sign error
+    // even when its triple is dropped (strtonum.h:416, libfm_parser.h:104)
+    for (uint64_t m = soF; m; m &= m - 1) {
+      const uint64_t q = P + ctz64(m);
+      if (sh.c.text[q - t.tlo + kPre] == '-') raise_error(a.err, E_NEG_INDEX, q);
+    }
+    // each index's field: the run before it (scanned back over the LDS masks)
+    uint64_t r = eI;
+    for (uint64_t m = so.I; m; m &= m - 1, ++r) {
+      const uint64_t q = P + ctz64(m);
+      const uint64_t f0 = t.floor_of(q);
+      const uint64_t fe = t.last_bit(0, f0, q);
+      const uint64_t x = fe == kNone ? kNone : t.last_bit(1, f0, fe);
+      const uint64_t fs = x == kNone ? f0 : x + 1;
+      const uint64_t lim = lim_of(fs);
+      uint64_t v = 0;
+      bool ok = false, pos = true;
+      if (fs + kPre >= t.tlo && fs + 16 <= lim) {
+        const W16 wq = win_at(sh.c.text, t.tlo, fs);
+        const uint32_t w4[4] = {(uint32_t)wq.lo, (uint32_t)(wq.lo >> 32), (uint32_t)wq.hi, (uint32_t)(wq.hi >> 32)};
+        pos = wuint32(w4, sh.dt, &v, &ok);
+      }
+      if (!ok) pos = slow_uint(a.text, fs, lim, a.wide, &v);
+      if (!pos) v = 0;  // raised by the field's owner above
+      if (a.indexing_mode > 0) --v;
+      if (r < a.cap[C_FIELD]) {
+        if (a.wide) reinterpret_cast<uint64_t *>(a.field)[r] = v;
+        else reinterpret_cast<uint32_t *>(a.field)[r] = (uint32_t)v;
+      } else {
+        raise_error(a.err, E_CAPACITY, q);
+      }
+    }
+  }
   FAST_STAMP(k, 6);
   // ---- per-chunk exclusive counts at each chunk start in my segment
   if (a.chunk_tab) {
@@ -522,7 +682,7 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
       row[C_WEIGHT] = eW + popc64(so.W & below);
       row[C_QID] = 0;
       row[C_LABEL] = rows;
-      row[C_FIELD] = 0;
+      row[C_FIELD] = FM ? row[C_INDEX] : 0;
     }
   }
 }

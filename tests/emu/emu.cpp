@@ -163,16 +163,19 @@ extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *c
   unsigned long long *err = reinterpret_cast<unsigned long long *>(res + 8);
   if (!ntiles && !count_only && out->offset) out->offset[0] = 0;
   if (!count_only) chunk_prefill(chunk_table, nchunks);
-  if (prm->format == DMLC_AMD_LIBSVM) {
-    // mirrors launch_libsvm (libsvm.hip): uniform-grammar kernel first, exact
-    // tile kernels when it sets the gate (or indexing_mode < 0 / FLAG_EXACT)
+  if (prm->format == DMLC_AMD_LIBSVM || prm->format == DMLC_AMD_LIBFM) {
+    // mirrors launch_libsvm (libsvm.hip) / launch_libfm (libfm.hip): the
+    // uniform-grammar kernel first, the exact tile kernels when it sets the
+    // gate (or indexing_mode < 0 / FLAG_EXACT)
+    const bool fm = prm->format == DMLC_AMD_LIBFM;
     const bool use_fast = nbytes > 0 && prm->indexing_mode >= 0 && !(prm->flags & DMLC_AMD_FLAG_EXACT);
     const uint64_t nft = (nbytes + fsvm::kTile - 1) / fsvm::kTile;
     uint32_t gate = use_fast ? 0u : 1u;
     unsigned long long ferr = ~0ull;
     std::vector<uint64_t> lb(nft * 8 + 1, 0);
-    LibsvmArgs a;
+    LibfmArgs a;
     std::memset(&a, 0, sizeof(a));
+    a.field = out->field;
     a.text = text;
     a.n = nbytes;
     a.cs = cs;
@@ -208,6 +211,7 @@ extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *c
       f.label = a.label;
       f.weight = a.weight;
       f.index = a.index;
+      f.field = fm ? out->field : nullptr;
       f.value = a.value;
       for (int i = 0; i < 8; ++i) f.cap[i] = out->cap[i];
       f.chunk_tab = chunk_table;
@@ -218,8 +222,15 @@ extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *c
       for (uint64_t k = 0; k < nft; ++k) {
         fsvm::Shared *sh = new fsvm::Shared;
         std::memset(sh, 0xCD, sizeof(*sh));
-        if (count_only) run_block([&](HostBlock &bk) { fsvm::tile<1>(f, *sh, bk, (uint32_t)k); });
-        else run_block([&](HostBlock &bk) { fsvm::tile<2>(f, *sh, bk, (uint32_t)k); });
+        run_block([&](HostBlock &bk) {
+          if (fm) {
+            if (count_only) fsvm::tile<1, true>(f, *sh, bk, (uint32_t)k);
+            else fsvm::tile<2, true>(f, *sh, bk, (uint32_t)k);
+          } else {
+            if (count_only) fsvm::tile<1>(f, *sh, bk, (uint32_t)k);
+            else fsvm::tile<2>(f, *sh, bk, (uint32_t)k);
+          }
+        });
         delete sh;
       }
     }
@@ -227,7 +238,10 @@ extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *c
       for (uint64_t k = 0; k < ntiles; ++k) {
         svm::Shared *sh = new svm::Shared;
         std::memset(sh, 0xCD, sizeof(*sh));  // LDS is uninitialised on the GPU
-        run_block([&](HostBlock &bk) { svm::tile<1>(a, *sh, bk, k); });
+        run_block([&](HostBlock &bk) {
+          if (fm) fm::tile<1>(a, *sh, bk, k);
+          else svm::tile<1>(a, *sh, bk, k);
+        });
         delete sh;
       }
       tile_scan(tile_cnt, tile_base, ntiles, res);
@@ -236,13 +250,16 @@ extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *c
         for (uint64_t k = 0; k < ntiles; ++k) {
           svm::Shared *sh = new svm::Shared;
           std::memset(sh, 0xCD, sizeof(*sh));
-          run_block([&](HostBlock &bk) { svm::tile<2>(a, *sh, bk, k); });
+          run_block([&](HostBlock &bk) {
+            if (fm) fm::tile<2>(a, *sh, bk, k);
+            else svm::tile<2>(a, *sh, bk, k);
+          });
           delete sh;
         }
     } else {
       res[8] = ferr;
     }
-    std::fprintf(stderr, "emu: libsvm path=%s\n", gate ? "exact" : "fast");
+    std::fprintf(stderr, "emu: %s path=%s\n", fm ? "libfm" : "libsvm", gate ? "exact" : "fast");
   } else if (prm->format == DMLC_AMD_CSV) {
     CsvArgs a;
     std::memset(&a, 0, sizeof(a));
@@ -341,44 +358,6 @@ extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *c
         csv::Shared *sh = new csv::Shared;
         std::memset(sh, 0xCD, sizeof(*sh));
         run_block([&](HostBlock &bk) { csv::tile<2>(a, *sh, bk, k); });
-        delete sh;
-      }
-  } else if (prm->format == DMLC_AMD_LIBFM) {  // mirrors launch_libfm (libfm.hip)
-    LibfmArgs a;
-    std::memset(&a, 0, sizeof(a));
-    a.text = text;
-    a.n = nbytes;
-    a.cs = cs;
-    a.nchunk = nchunks;
-    a.tile_bytes = T;
-    a.ntiles = (uint32_t)ntiles;
-    a.wide = prm->index_bits == 64;
-    a.indexing_mode = prm->indexing_mode;
-    a.tile_cnt = tile_cnt.data();
-    a.tile_base = tile_base.data();
-    a.offset = out->offset;
-    a.label = reinterpret_cast<float *>(out->label);
-    a.weight = out->weight;
-    a.index = out->index;
-    a.field = out->field;
-    a.value = reinterpret_cast<float *>(out->value);
-    for (int i = 0; i < 8; ++i) a.cap[i] = out->cap[i];
-    a.chunk_tab = chunk_table ? chunk_table : sink.data();
-    a.chunk_min = chunk_min.data();
-    a.err = err;
-    for (uint64_t k = 0; k < ntiles; ++k) {
-      svm::Shared *sh = new svm::Shared;
-      std::memset(sh, 0xCD, sizeof(*sh));
-      run_block([&](HostBlock &bk) { fm::tile<1>(a, *sh, bk, k); });
-      delete sh;
-    }
-    tile_scan(tile_cnt, tile_base, ntiles, res);
-    if (!count_only && out->offset && res[C_ROWS] < out->cap[C_ROWS] + 1) out->offset[res[C_ROWS]] = res[C_INDEX];
-    if (!count_only)
-      for (uint64_t k = 0; k < ntiles; ++k) {
-        svm::Shared *sh = new svm::Shared;
-        std::memset(sh, 0xCD, sizeof(*sh));
-        run_block([&](HostBlock &bk) { fm::tile<2>(a, *sh, bk, k); });
         delete sh;
       }
   } else {

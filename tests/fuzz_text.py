@@ -162,3 +162,35 @@ def labeled_csv(rng, nlines, ncols, label_col, delim=",", defects=0.0):
                 fields.append("")
         out.append(delim.join(fields))
     return ("\n".join(out) + "\n").encode()
+
+
+def uniform_libfm(rng, nlines, maxtrip=20, violate=False):
+    """libfm lines in the single-pass kernel's grammar (digitchars, blanks, ':'
+    and newlines): label[:weight], field:index[:value] groups, dropped lone
+    fields, pairs without values, blank lines; violate=True also injects
+    structures that leave it ("a:b:c:d", "l:w:x", dangling "f:", signs)."""
+    lines = []
+    for _ in range(nlines):
+        if rng.random() < 0.05:
+            lines.append(" " * int(rng.integers(0, 3)))
+            continue
+        head = str(int(rng.integers(0, 3)))
+        if rng.random() < 0.2:
+            head += ":%.4g" % float(rng.random())
+        parts = [head]
+        for _ in range(int(rng.integers(0, maxtrip + 1))):
+            f, i = int(rng.integers(0, 50)), int(rng.integers(0, 3000))
+            r = rng.random()
+            if r < 0.1:
+                parts.append("%d" % f)  # lone field: dropped (r = 1)
+            elif r < 0.25:
+                parts.append("%d:%d" % (f, i))  # no value (r = 2)
+            else:
+                parts.append("%d:%d:%.9g" % (f, i, float(rng.random()) * (10 ** int(rng.integers(-2, 4)))))
+        if violate and rng.random() < 0.3:
+            parts.append(["1:2:3:4", "-3:4:5", "7:", "+2:3:4", "5:-6:1"][int(rng.integers(0, 5))])
+        sep = " " * int(rng.integers(1, 3)) if rng.random() < 0.2 else " "
+        lines.append(sep.join(parts))
+    ends = ["\n"] * 10 + ["\r\n", "\n\n"]
+    text = "".join(l + ends[int(rng.integers(0, len(ends)))] for l in lines)
+    return text.encode()

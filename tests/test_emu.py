@@ -230,3 +230,27 @@ def test_emu_csv_fast_label_column():
             assert h["path"] == "fast", it
         fast += h["path"] == "fast"
     assert fast >= 12
+
+
+def test_emu_libfm_fast_vs_oracle():
+    """libfm through the single-pass kernel (svm_fast.h with the libfm roles):
+    clean uniform inputs stay on it; violations go exact; the reference's
+    result or error either way, chunk tables included."""
+    rng = np.random.default_rng(515)
+    paths = {"fast": 0, "exact": 0}
+    for it in range(40):
+        big = it % 8 == 7
+        data = fuzz_text.uniform_libfm(rng, 600 if big else int(rng.integers(1, 30)), 20 if big else 8,
+                                       violate=it % 3 == 2)
+        offs = fuzz_text.random_cuts(rng, data, 5, anywhere=it % 5 == 4)
+        kw = {"indexing_mode": 1} if it % 4 == 1 else {}
+        o = po.parse_chunks(data, offs, fmt=po.LIBFM, **kw)
+        h = pyemu.parse(data, offs, "libfm", **kw)
+        failed = check_fail(h, "libfm", offs)
+        assert (o["status"] != 0) == failed, (it, data[:300], offs, o["msg"], h["error"])
+        if not failed:
+            assert diff(h, o) == [], (it, diff(h, o), offs)
+        paths[h["path"]] += 1
+        if it % 3 != 2 and it % 5 != 4:
+            assert h["path"] == "fast", (it, data[:300])
+    assert paths["fast"] >= 15 and paths["exact"] >= 3, paths

@@ -95,7 +95,7 @@ def test_gpu_synthetic_config1(dm, name):
 
 
 def _oracle_vs_gpu(dm, data, offs, fmt, **kw):
-    okw = {("value_kind" if k == "value_type" else k): v for k, v in kw.items() if k != "tile_bytes"}
+    okw = {("value_kind" if k == "value_type" else k): v for k, v in kw.items() if k not in ("tile_bytes", "exact")}
     o = po.parse_chunks(data, offs, fmt=fmt, **okw)
     h = gpu_parse(dm, data, offs, fmt, **kw)
     assert (o["status"] != 0) == h["failed"], (o["msg"], h["error"])
@@ -409,7 +409,11 @@ def test_gpu_libfm_synthetic_vs_oracle(dm):
     assert len(data) > 1 << 20
     for kw in ({}, {"indexing_mode": 1}, {"indexing_mode": -1}, {"index_bits": 64, "tile_bytes": 4096}):
         h = _oracle_vs_gpu(dm, data, _random_chunks(rng, data, 12), po.LIBFM, **kw)
-        assert h["path"] == "exact" and len(h["field"]) == len(h["index"]) > 100000
+        # the single-pass kernel unless indexing_mode < 0 (per-chunk detection)
+        assert h["path"] == ("exact" if kw.get("indexing_mode", 0) < 0 else "fast"), kw
+        assert len(h["field"]) == len(h["index"]) > 100000
+        he = _oracle_vs_gpu(dm, data, [0, len(data)], po.LIBFM, exact=True, **kw)
+        assert he["path"] == "exact"
 
 
 @pytest.mark.gpu
@@ -435,3 +439,27 @@ def test_gpu_csv_fast_label_column_vs_oracle(dm):
     for lc in (0, 5):
         h = _oracle_vs_gpu(dm, text.tobytes(), offs, po.CSV, label_column=lc)
         assert h["path"] == "fast" and len(h["label"]) == 6000 and len(h["index"]) == 6000 * 255
+
+
+@pytest.mark.gpu
+def test_gpu_libfm_fast_fuzz_vs_oracle(dm):
+    """Uniform-grammar libfm (pairs without values, dropped lone fields,
+    weights, CR/LF, chunk cuts anywhere) through the single-pass kernel and
+    violations through the exact kernels: the reference's result or error."""
+    rng = np.random.default_rng(717)
+    paths = {"fast": 0, "exact": 0}
+    for it in range(200):
+        big = it % 10 == 9
+        data = fuzz_text.uniform_libfm(rng, 2000 if big else int(rng.integers(1, 60)), 24 if big else 10,
+                                       violate=it % 3 == 2)
+        offs = fuzz_text.random_cuts(rng, data, 8, anywhere=it % 5 == 4)
+        kw = {}
+        if it % 4 == 1:
+            kw["indexing_mode"] = 1
+        if it % 7 == 3:
+            kw["index_bits"] = 64
+        h = _oracle_vs_gpu(dm, data, offs, po.LIBFM, **kw)
+        paths[h["path"]] += 1
+        if it % 3 != 2 and it % 5 != 4:
+            assert h["path"] == "fast", it
+    assert paths["fast"] >= 90 and paths["exact"] >= 30, paths
