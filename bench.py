@@ -45,7 +45,7 @@ DESC = {
     "csv_1m_x256": "CSV dense 1M rows x 256 float cols, device-resident",
     "libsvm_1m_x2048": "libsvm 1M rows x 2048 nnz/row, device-resident",
     "libsvm_32m_x64": "libsvm 32M rows x 64 nnz/row, chunks sharded across GPUs",
-    "libfm_1m_x64": "libfm 1M rows x 64 field:id:value/row, device-resident (exact kernels)",
+    "libfm_1m_x64": "libfm 1M rows x 64 field:id:value/row, device-resident",
 }
 
 
