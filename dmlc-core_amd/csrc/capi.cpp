@@ -68,10 +68,10 @@ void prof_mark(int end, hipStream_t s, const char *kernel) {
         p.ev.push_back(e);
       }
     }
-    hipEventRecord(p.ev[p.used], s);
+    (void)hipEventRecord(p.ev[p.used], s);
     p.kernel = kernel;
   } else {
-    hipEventRecord(p.ev[p.used + 1], s);
+    (void)hipEventRecord(p.ev[p.used + 1], s);
     p.used += 2;
   }
 }

@@ -171,6 +171,8 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
   t.sh = &sh;
   t.tlo = (uint64_t)k * kTile;
   t.thi = mn<uint64_t>(t.tlo + kTile, a.n);
+  StageRegs sr;
+  stage_issue(a.text, a.n, t.tlo, sr, bk);  // text loads first: the chunk search overlaps them
   if (tid < kWave) chunk_list(a.cs, a.nchunk, t.tlo, t.thi, sh.c, bk);
   if (tid == 0) {
     sh.md[0] = sh.mn[0] = sh.ml[0] = 0;
@@ -178,7 +180,7 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
   }
   sh.cls[tid] = class_of_csv((uint32_t)tid, a.delim);
   init_dec_tables(sh.dt, bk);
-  stage(a.text, a.n, t.tlo, sh.c, bk);
+  stage_commit(a.text, a.n, t.tlo, sr, sh.c, bk);
   bk.sync();
   // ---- classify: segment tid -> slot tid+1; lanes 0..15 also one dword
   // each of the 64 bytes before the tile -> slot 0

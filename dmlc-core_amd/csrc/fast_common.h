@@ -586,6 +586,48 @@ DA_HDF void stage(const uint8_t *text, uint64_t n, uint64_t tlo, TileCommon &c, 
   }
 }
 
+// The same staging split in two so every load of the tile is in flight at
+// once: stage_issue loads each thread's 16-byte units into registers (all
+// kStageRounds loads before any wait), stage_commit writes them to LDS.  The
+// caller puts the tile's other prologue work (chunk list, tables) between the
+// two, so its latency overlaps the loads'.  (A single loop of load -> LDS
+// store waited for each load in turn: 5 HBM round trips per tile, ~14k cycles
+// of a ~57k-cycle tile.)  Tiles whose staged range leaves the text take the
+// byte-wise path of stage() at commit time.
+constexpr int kStageUnits = kStage / 16;
+constexpr int kStageRounds = (kStageUnits + kThreads - 1) / kThreads;
+static_assert(kStage % 16 == 0, "staged range is whole 16-byte units");
+struct StageRegs {
+  uint32_t w[kStageRounds][4];
+  bool interior;
+};
+template <class BK>
+DA_HDF void stage_issue(const uint8_t *text, uint64_t n, uint64_t tlo, StageRegs &r, BK &bk) {
+  r.interior = tlo >= (uint64_t)kPre && tlo + kTile + kPost <= n;
+  if (!r.interior) return;
+  const uint8_t *src = text + (tlo - kPre);
+  const int t = bk.tid();
+#pragma unroll
+  for (int i = 0; i < kStageRounds; ++i) {
+    const int u = t + i * kThreads;
+    if (u < kStageUnits) load16(src + 16 * u, r.w[i]);
+  }
+}
+template <class BK>
+DA_HDF void stage_commit(const uint8_t *text, uint64_t n, uint64_t tlo, const StageRegs &r, TileCommon &c,
+                         BK &bk) {
+  if (!r.interior) {
+    stage(text, n, tlo, c, bk);
+    return;
+  }
+  const int t = bk.tid();
+#pragma unroll
+  for (int i = 0; i < kStageRounds; ++i) {
+    const int u = t + i * kThreads;
+    if (u < kStageUnits) memcpy(c.text + 16 * u, r.w[i], 16);
+  }
+}
+
 // ---- decoupled look-back records: 8 words (one 64-byte line) per tile.
 // Word 0 = status (bits 62-63: 1 aggregate, 2 inclusive) | the tile's four
 // counts packed 15 bits each (a 16 KiB tile holds < 2^15 of anything);

@@ -380,11 +380,13 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
   t.sh = &sh;
   t.tlo = (uint64_t)k * kTile;
   t.thi = mn<uint64_t>(t.tlo + kTile, a.n);
+  StageRegs sr;
+  stage_issue(a.text, a.n, t.tlo, sr, bk);  // text loads first: the chunk search overlaps them
   if (tid < kWave) chunk_list(a.cs, a.nchunk, t.tlo, t.thi, sh.c, bk);
   if (tid == 0) sh.md[0] = sh.mn[0] = sh.mc[0] = 0;
   sh.cls[tid] = class_of((uint32_t)tid);
   init_dec_tables(sh.dt, bk);
-  stage(a.text, a.n, t.tlo, sh.c, bk);
+  stage_commit(a.text, a.n, t.tlo, sr, sh.c, bk);
   bk.sync();
   FAST_STAMP(k, 2);
 #if defined(FSVM_ABL_STOP) && FSVM_ABL_STOP == 0  // timing ablation only: stage
