@@ -173,7 +173,8 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
   t.thi = mn<uint64_t>(t.tlo + kTile, a.n);
   StageRegs sr;
   stage_issue(a.text, a.n, t.tlo, sr, bk);  // text loads first: the chunk search overlaps them
-  if (tid < kWave) chunk_list(a.cs, a.nchunk, t.tlo, t.thi, sh.c, bk);
+  ChunkProbe cp;  // wave 0: the window load stays in flight through classification
+  if (tid < kWave) cp = chunk_list_begin(a.cs, a.nchunk, t.tlo, bk);
   if (tid == 0) {
     sh.md[0] = sh.mn[0] = sh.ml[0] = 0;
     sh.nlab = sh.nfirst = 0;
@@ -215,9 +216,10 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
       atomic_or_u64(&sh.mn[0], (uint64_t)b.n << (4 * tid));
       atomic_or_u64(&sh.ml[0], (uint64_t)b.c << (4 * tid));
     }
-    if (tid == 0) bad |= sh.c.toomany;
   }
+  if (tid < kWave) chunk_list_end(a.cs, a.nchunk, t.tlo, t.thi, cp, sh.c, bk);
   bk.sync();
+  if (tid == 0) bad |= sh.c.toomany;
   // ---- rows, fields, tokens of my segment
   const uint64_t P = t.tlo + (uint64_t)tid * kSegB;
   uint64_t RS = 0, T = 0, L = 0;

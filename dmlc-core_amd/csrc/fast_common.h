@@ -512,9 +512,15 @@ struct TileCommon {
 // (9 loads at 257 chunks, the longest latency of the tile prologue) -- and the
 // list comes from one more window load: csl = cs[c_first ..] inside [tlo, thi]
 // (excluding cs[nchunk]), cnext = the entry after the list (cs[nchunk] == n).
+//
+// Split in two so the last load's latency overlaps other prologue work:
+// chunk_list_begin runs the search rounds and issues the window load,
+// chunk_list_end consumes it (the caller classifies in between).
+struct ChunkProbe {
+  uint64_t lo, cnt, v;
+};
 template <class BK>
-DA_HDF void chunk_list(const uint64_t *cs, int nchunk, uint64_t tlo, uint64_t thi, TileCommon &c,
-                       BK &bk) {
+DA_HDF ChunkProbe chunk_list_begin(const uint64_t *cs, int nchunk, uint64_t tlo, BK &bk) {
   const uint32_t lane = (uint32_t)bk.tid();
   const uint64_t kBig = ~0ull;
   // invariant: cs[lo] <= tlo, the answer (last i < nchunk with cs[i] <= tlo) lies in [lo, lo + cnt)
@@ -530,7 +536,19 @@ DA_HDF void chunk_list(const uint64_t *cs, int nchunk, uint64_t tlo, uint64_t th
     lo = nlo;
   }
   // window cs[lo .. lo + 64) (entries past cs[nchunk] read as "beyond")
-  uint64_t v = lo + lane <= (uint64_t)nchunk ? cs[lo + lane] : kBig;
+  ChunkProbe p;
+  p.lo = lo;
+  p.cnt = cnt;
+  p.v = lo + lane <= (uint64_t)nchunk ? cs[lo + lane] : kBig;
+  return p;
+}
+template <class BK>
+DA_HDF void chunk_list_end(const uint64_t *cs, int nchunk, uint64_t tlo, uint64_t thi, const ChunkProbe &p,
+                           TileCommon &c, BK &bk) {
+  const uint32_t lane = (uint32_t)bk.tid();
+  const uint64_t kBig = ~0ull;
+  uint64_t lo = p.lo, v = p.v;
+  const uint64_t cnt = p.cnt;
   uint64_t m = bk.ballot(lane < cnt && v <= tlo);
   const uint64_t c0 = lo + (63 - clz64(m));
   if (c0 - lo > (uint64_t)(kWave - kMaxCs - 2)) {  // the list may run past the window: reload at c0
@@ -554,6 +572,12 @@ DA_HDF void chunk_list(const uint64_t *cs, int nchunk, uint64_t tlo, uint64_t th
     c.toomany = over;
     c.bad = 0;
   }
+}
+template <class BK>
+DA_HDF void chunk_list(const uint64_t *cs, int nchunk, uint64_t tlo, uint64_t thi, TileCommon &c,
+                       BK &bk) {
+  const ChunkProbe p = chunk_list_begin(cs, nchunk, tlo, bk);
+  chunk_list_end(cs, nchunk, tlo, thi, p, c, bk);
 }
 
 // All threads: stage [tlo - kPre, tlo + kTile + kPost) into LDS with 16-byte

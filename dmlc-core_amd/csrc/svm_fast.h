@@ -382,7 +382,8 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
   t.thi = mn<uint64_t>(t.tlo + kTile, a.n);
   StageRegs sr;
   stage_issue(a.text, a.n, t.tlo, sr, bk);  // text loads first: the chunk search overlaps them
-  if (tid < kWave) chunk_list(a.cs, a.nchunk, t.tlo, t.thi, sh.c, bk);
+  ChunkProbe cp;  // wave 0: the window load stays in flight through classification
+  if (tid < kWave) cp = chunk_list_begin(a.cs, a.nchunk, t.tlo, bk);
   if (tid == 0) sh.md[0] = sh.mn[0] = sh.mc[0] = 0;
   sh.cls[tid] = class_of((uint32_t)tid);
   init_dec_tables(sh.dt, bk);
@@ -423,9 +424,10 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
       atomic_or_u64(&sh.mn[0], (uint64_t)b.n << (4 * tid));
       atomic_or_u64(&sh.mc[0], (uint64_t)b.c << (4 * tid));
     }
-    if (tid == 0) bad |= sh.c.toomany;
   }
+  if (tid < kWave) chunk_list_end(a.cs, a.nchunk, t.tlo, t.thi, cp, sh.c, bk);
   bk.sync();
+  if (tid == 0) bad |= sh.c.toomany;
   FAST_STAMP(k, 3);
 #if defined(FSVM_ABL_STOP) && FSVM_ABL_STOP == 1  // timing ablation only: stage + classify
   if (sh.md[tid + 1] == 0x123456789ull) a.res[15] = sh.mn[tid];
