@@ -3,13 +3,26 @@
 #pragma once
 #include <stdint.h>
 
+#include "hd.h"
+
 namespace dmlc_amd {
+
+// ParseBlock units and InputSplit chunks.  `cs` lists the ParseBlock units
+// (text_parser.h:116-155 FillData: each chunk cut into nthread ranges); the
+// number decoders read on to the end of the InputSplit CHUNK holding a unit,
+// as the reference's strtof / atoll / ParseTriple do over the chunk buffer
+// (lcs = chunk starts, ldiv = units per chunk).
+struct UnitLim {
+  const uint64_t *lcs;
+  int ldiv;
+  DA_HD uint64_t lim(int unit) const { return lcs[(ldiv == 1 ? unit : unit / ldiv) + 1]; }
+};
 
 struct LibsvmArgs {
   const uint8_t *text;
   uint64_t n;
-  const uint64_t *cs;  // chunk starts, nchunk + 1 entries, cs[nchunk] == n
-  int nchunk;
+  const uint64_t *cs;  // ParseBlock unit starts, nchunk + 1 entries, cs[nchunk] == n
+  int nchunk;          // units
   uint64_t tile_bytes;
   uint32_t ntiles;
   int wide;            // IndexType is uint64_t
@@ -27,6 +40,8 @@ struct LibsvmArgs {
   uint64_t *chunk_min;  // [nchunk] min index per chunk (indexing_mode < 0)
   unsigned long long *err;
   const uint32_t *gate;  // when set, the tile kernels run only if *gate != 0
+  UnitLim ul;            // decoder limit per unit
+  DA_HD uint64_t lim(int unit) const { return ul.lim(unit); }
 };
 
 // libfm exact tile kernels (libfm_core.h): the libsvm block plus field ids.
@@ -107,6 +122,8 @@ struct CsvArgs {
   uint64_t *chunk_tab;
   unsigned long long *err;
   const uint32_t *gate;  // when set, the tile kernels run only if *gate != 0
+  UnitLim ul;            // decoder limit per unit
+  DA_HD uint64_t lim(int unit) const { return ul.lim(unit); }
 };
 
 }  // namespace dmlc_amd

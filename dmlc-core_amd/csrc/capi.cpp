@@ -125,13 +125,18 @@ const char *dmlc_amd_error_string(int code) {
   }
 }
 
+// FillData ranges per chunk (dmlc_amd_params.nthread; 0 = 1)
+int units_per_chunk(const dmlc_amd_params *p) { return p && p->nthread > 1 ? p->nthread : 1; }
+constexpr int kMaxNthread = 1 << 12;
+
 size_t dmlc_amd_workspace_bytes(uint64_t nbytes, int nchunks, const dmlc_amd_params *prm) {
   const uint64_t T = tile_of(prm);
   const uint64_t ntiles = (nbytes + T - 1) / T;
-  const uint64_t nc = nchunks > 0 ? (uint64_t)nchunks : 1;
+  const uint64_t nc = (nchunks > 0 ? (uint64_t)nchunks : 1) * (uint64_t)units_per_chunk(prm);
   const uint64_t nft = (nbytes + kFastTile - 1) / kFastTile;
-  return (size_t)((2 * ntiles * kSlots + nc + nc * 8 + nft * 8 + dmlc_amd::kLabShards * 8) * sizeof(uint64_t) +
-                  11 * 256);
+  return (size_t)((2 * ntiles * kSlots + nc + nc * 8 + (nc + 1) + nft * 8 + dmlc_amd::kLabShards * 8) *
+                      sizeof(uint64_t) +
+                  12 * 256);
 }
 
 int dmlc_amd_parse(const void *d_text, uint64_t nbytes, const uint64_t *d_chunk_starts, int nchunks,
@@ -147,24 +152,42 @@ int dmlc_amd_parse(const void *d_text, uint64_t nbytes, const uint64_t *d_chunk_
   if (prm->format == DMLC_AMD_CSV && prm->label_column >= 0 &&
       prm->label_column == prm->weight_column)
     return DMLC_AMD_ERR_ARG;  // csv_parser.h:59-60
+  if (prm->nthread < 0 || prm->nthread > kMaxNthread) return DMLC_AMD_ERR_ARG;
   if (workspace_bytes < dmlc_amd_workspace_bytes(nbytes, nchunks, prm) || !d_workspace)
     return DMLC_AMD_ERR_ARG;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const uint64_t T = tile_of(prm);
   const uint64_t ntiles = (nbytes + T - 1) / T;
-  const int nc = nchunks > 0 ? nchunks : 1;
+  const int upc = units_per_chunk(prm);
+  const uint64_t nunits = (uint64_t)(nchunks > 0 ? nchunks : 0) * (uint64_t)upc;
+  if (nunits > (uint64_t)INT32_MAX) return DMLC_AMD_ERR_ARG;
+  const int nc = nunits > 0 ? (int)nunits : 1;
   Carve cv{reinterpret_cast<char *>(d_workspace), workspace_bytes};
   uint64_t *tile_cnt = cv.take<uint64_t>(ntiles * kSlots + 1);
   uint64_t *tile_base = cv.take<uint64_t>(ntiles * kSlots + 1);
   uint64_t *chunk_min = cv.take<uint64_t>(nc);
   uint64_t *chunk_sink = cv.take<uint64_t>((size_t)nc * 8);
+  uint64_t *units = cv.take<uint64_t>((size_t)nc + 1);  // ParseBlock unit starts (nthread > 1)
   const uint64_t nft = (nbytes + kFastTile - 1) / kFastTile;
-  uint32_t *ctl = cv.take<uint32_t>(4);               // gate
+  uint32_t *ctl = cv.take<uint32_t>(4);               // gate, gate after the count phase, recount flag
   unsigned long long *ferr = cv.take<unsigned long long>(1);
   uint64_t *lb = cv.take<uint64_t>(nft * 8 + 1);
   uint64_t *labsum = cv.take<uint64_t>(dmlc_amd::kLabShards * 8);
-  if (!tile_cnt || !tile_base || !chunk_min || !chunk_sink || !ctl || !ferr || !lb || !labsum)
+  if (!tile_cnt || !tile_base || !chunk_min || !chunk_sink || !units || !ctl || !ferr || !lb || !labsum)
     return DMLC_AMD_ERR_ARG;
+  // FillData's thread ranges become the units the kernels parse; the
+  // decoders still read to the end of the InputSplit chunk (args.h UnitLim)
+  const uint64_t *ucs = d_chunk_starts;
+  if (upc > 1 && nbytes > 0) {
+    const hipError_t re = dmlc_amd::launch_ranges(reinterpret_cast<const uint8_t *>(d_text), d_chunk_starts,
+                                                  nchunks, upc, nbytes, units, s);
+    if (re != hipSuccess) {
+      g_last_hip = re;
+      return DMLC_AMD_ERR_HIP;
+    }
+    ucs = units;
+  }
+  const dmlc_amd::UnitLim ul{d_chunk_starts, upc};
   uint64_t *res = reinterpret_cast<uint64_t *>(d_result);
   const bool count_only = (prm->flags & DMLC_AMD_FLAG_COUNT_ONLY) != 0;
   const bool fill_only = (prm->flags & DMLC_AMD_FLAG_FILL_ONLY) != 0;
@@ -177,8 +200,9 @@ int dmlc_amd_parse(const void *d_text, uint64_t nbytes, const uint64_t *d_chunk_
     std::memset(&a, 0, sizeof(a));
     a.text = reinterpret_cast<const uint8_t *>(d_text);
     a.n = nbytes;
-    a.cs = d_chunk_starts;
-    a.nchunk = nchunks;
+    a.cs = ucs;
+    a.nchunk = (int)nunits;
+    a.ul = ul;
     a.tile_bytes = T;
     a.ntiles = (uint32_t)ntiles;
     a.wide = prm->index_bits == 64;
@@ -200,8 +224,8 @@ int dmlc_amd_parse(const void *d_text, uint64_t nbytes, const uint64_t *d_chunk_
     std::memset(&f, 0, sizeof(f));
     f.text = a.text;
     f.n = nbytes;
-    f.cs = d_chunk_starts;
-    f.nchunk = nchunks;
+    f.cs = ucs;
+    f.nchunk = (int)nunits;
     f.ntiles = (uint32_t)nft;
     f.wide = a.wide;
     f.indexing_mode = prm->indexing_mode;
@@ -224,8 +248,9 @@ int dmlc_amd_parse(const void *d_text, uint64_t nbytes, const uint64_t *d_chunk_
     std::memset(&a, 0, sizeof(a));
     a.text = reinterpret_cast<const uint8_t *>(d_text);
     a.n = nbytes;
-    a.cs = d_chunk_starts;
-    a.nchunk = nchunks;
+    a.cs = ucs;
+    a.nchunk = (int)nunits;
+    a.ul = ul;
     a.tile_bytes = T;
     a.ntiles = (uint32_t)ntiles;
     a.wide = prm->index_bits == 64;
@@ -249,8 +274,8 @@ int dmlc_amd_parse(const void *d_text, uint64_t nbytes, const uint64_t *d_chunk_
     std::memset(&f, 0, sizeof(f));
     f.text = a.text;
     f.n = nbytes;
-    f.cs = d_chunk_starts;
-    f.nchunk = nchunks;
+    f.cs = ucs;
+    f.nchunk = (int)nunits;
     f.ntiles = (uint32_t)nft;
     f.wide = a.wide;
     f.delim = a.delim;
@@ -277,8 +302,9 @@ int dmlc_amd_parse(const void *d_text, uint64_t nbytes, const uint64_t *d_chunk_
     std::memset(&a, 0, sizeof(a));
     a.text = reinterpret_cast<const uint8_t *>(d_text);
     a.n = nbytes;
-    a.cs = d_chunk_starts;
-    a.nchunk = nchunks;
+    a.cs = ucs;
+    a.nchunk = (int)nunits;
+    a.ul = ul;
     a.tile_bytes = T;
     a.ntiles = (uint32_t)ntiles;
     a.wide = prm->index_bits == 64;
@@ -300,8 +326,8 @@ int dmlc_amd_parse(const void *d_text, uint64_t nbytes, const uint64_t *d_chunk_
     std::memset(&f, 0, sizeof(f));
     f.text = a.text;
     f.n = nbytes;
-    f.cs = d_chunk_starts;
-    f.nchunk = nchunks;
+    f.cs = ucs;
+    f.nchunk = (int)nunits;
     f.ntiles = (uint32_t)nft;
     f.wide = a.wide;
     f.indexing_mode = prm->indexing_mode;

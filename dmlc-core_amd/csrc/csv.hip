@@ -102,8 +102,20 @@ hipError_t launch_csv(const CsvArgs &a, const FastCsvArgs &f, bool use_fast, uin
       csv_tile<1><<<a.ntiles, kThreads, 0, s>>>(a);
       tile_scan_kernel<<<1, kThreads, 0, s>>>(a.tile_cnt, const_cast<uint64_t *>(a.tile_base), a.ntiles,
                                               res, a.offset, a.cap[C_ROWS], gate);
+      if (phase == kPhaseCount) note_gate_kernel<<<1, 1, 0, s>>>(gate);
+    } else {
+      // the count phase stood on the single-pass kernel but its write pass
+      // handed over: count on the exact path first (scan.h recount_flag_kernel)
+      recount_flag_kernel<<<1, 1, 0, s>>>(gate);
+      auto ra = a;
+      ra.gate = gate + 2;
+      csv_tile<1><<<a.ntiles, kThreads, 0, s>>>(ra);
+      tile_scan_kernel<<<1, kThreads, 0, s>>>(a.tile_cnt, const_cast<uint64_t *>(a.tile_base), a.ntiles,
+                                              res, a.offset, a.cap[C_ROWS], gate + 2);
     }
     if (phase != kPhaseCount) {
+      if (use_fast && f.chunk_tab && f.nchunk > 0)
+        tab_reset_kernel<<<(f.nchunk * 8 + 255) / 256, 256, 0, s>>>(f.chunk_tab, (uint64_t)f.nchunk * 8, gate);
       if (!use_fast) prof_mark(0, s, "csv_tile<2>");
       csv_tile<2><<<a.ntiles, kThreads, 0, s>>>(a);
       if (!use_fast) prof_mark(1, s, "csv_tile<2>");

@@ -176,7 +176,7 @@ DA_HDF void walk(const CsvArgs &a, Src &src, const Seg &sg, uint32_t state, Cnt 
   uint32_t ev = sg.ls | sg.dl | sg.fs;
   int chunk = sg.chunk;
   uint64_t cend = a.cs[chunk + 1];
-  src.lim = cend;
+  src.lim = a.lim(chunk);  // decoders read to the InputSplit chunk end
   uint64_t col = state & 0x3FFFFFFFu;
   bool slow = (state >> 30) & 1u;
   bool in_line = (state >> 31) & 1u;  // a line start has been seen (always true inside an extent)
@@ -187,7 +187,7 @@ DA_HDF void walk(const CsvArgs &a, Src &src, const Seg &sg, uint32_t state, Cnt 
     while (x >= cend) {
       ++chunk;
       cend = a.cs[chunk + 1];
-      src.lim = cend;
+      src.lim = a.lim(chunk);  // decoders read to the InputSplit chunk end
     }
     if ((sg.ls >> i) & 1u) {
       in_line = true;
@@ -278,7 +278,7 @@ DA_HDF uint64_t first_line_start(const CsvArgs &a, BK &bk, uint64_t from, uint64
       int c = chunk_of(a.cs, a.nchunk, lo);
       for (uint64_t p = lo; p < hi; ++p) {
         while (p >= a.cs[c + 1]) ++c;
-        src.lim = a.cs[c + 1];
+        src.lim = a.lim(c);
         if (csv_line_start(src, p, a.cs[c])) {
           best = p;
           break;
@@ -353,7 +353,7 @@ DA_HDF void tile(const CsvArgs &a, Shared &sh, BK &bk, uint64_t k) {
     if (sg.lo < sg.hi) {
       sg.chunk = chunk_of(a.cs, a.nchunk, sg.lo);
       int c = sg.chunk;
-      src.lim = a.cs[c + 1];
+      src.lim = a.lim(c);
       const int len = (int)(sg.hi - sg.lo);
       uint32_t nl = 0, dl = 0, ls = 0;
       for (int i = 0; i < len; ++i) {
@@ -373,13 +373,13 @@ DA_HDF void tile(const CsvArgs &a, Shared &sh, BK &bk, uint64_t k) {
         m &= m - 1;
         const uint64_t x = sg.lo + i;
         while (x >= a.cs[c + 1]) ++c;
-        src.lim = a.cs[c + 1];
+        src.lim = a.lim(c);
         if (csv_line_start(src, x, a.cs[c])) {
           ls |= 1u << i;
           if (!a.fast_delim || is_bom_at(src, x)) sg.slow |= 1u << i;
         }
       }
-      src.lim = a.cs[sg.chunk + 1];
+      src.lim = a.lim(sg.chunk);
       sg.ls = ls;
       sg.dl = dl & ~nl;
       // field starts: line starts of fast lines, and bytes after a delimiter that are not nl

@@ -303,6 +303,9 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
   }
   // ---- decoupled look-back by wave 0
   if (tid < kWave) csv_look_back(a.lb, k, cnt4, a.gate, sh.c, bk, &sh.segc);
+#ifdef DMLC_AMD_VALVE_TEST  // test-only build (lib/variants): the write pass of tile 1 hands over
+  if (MODE == 2 && k == 1 && tid == 0) atomic_or_u32(a.gate, 2u);
+#endif
   bk.sync();
   const uint64_t bRows = sh.c.base[Q_ROWS], bVal = sh.c.base[Q_VALS], tcarry = sh.segc;
   // With a label column (csv_parser.h:111-112) the field at column label_col

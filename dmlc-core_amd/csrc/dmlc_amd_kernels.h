@@ -25,6 +25,10 @@ hipError_t launch_libsvm(const LibsvmArgs &a, const FastSvmArgs &f, bool use_fas
                          int phase, hipStream_t s);
 hipError_t launch_libfm(const LibfmArgs &a, const FastSvmArgs &f, bool use_fast, uint64_t *res, int phase,
                         hipStream_t s);
+// units[c * nthread + t] = start of FillData range t of chunk c
+// (text_parser.h:116-155); units[nchunk * nthread] = n.
+hipError_t launch_ranges(const uint8_t *text, const uint64_t *cs, int nchunk, int nthread, uint64_t n,
+                         uint64_t *units, hipStream_t s);
 hipError_t launch_csv(const CsvArgs &a, const FastCsvArgs &f, bool use_fast, uint64_t *res, int phase,
                       hipStream_t s);
 

@@ -91,7 +91,7 @@ DA_HDF void walk(const LibfmArgs &a, Src &src, const uint32_t *r1bits, uint64_t 
   uint32_t ev = sg.rs | sg.ls | sg.le;
   int chunk = sg.chunk;
   uint64_t cfloor = a.cs[chunk], cend = a.cs[chunk + 1];
-  src.lim = cend;
+  src.lim = a.lim(chunk);  // decoders read to the InputSplit chunk end
   // one (field, index) pair: decode, check signs, store / track the chunk minimum
   auto pair = [&](uint64_t fpos, uint64_t ipos, uint64_t x) {
     if (MODE == 2 || a.indexing_mode < 0) {
@@ -146,7 +146,7 @@ DA_HDF void walk(const LibfmArgs &a, Src &src, const uint32_t *r1bits, uint64_t 
       ++chunk;
       cfloor = a.cs[chunk];
       cend = a.cs[chunk + 1];
-      src.lim = cend;
+      src.lim = a.lim(chunk);  // decoders read to the InputSplit chunk end
     }
     if ((sg.ls >> i) & 1u) {
       if (MODE == 0) {
@@ -287,7 +287,7 @@ DA_HDF void tile(const LibfmArgs &a, svm::Shared &sh, BK &bk, uint64_t k) {
     sg.chunk = 0;
     if (sg.lo < sg.hi) {
       sg.chunk = chunk_of(a.cs, a.nchunk, sg.lo);
-      src.lim = a.cs[sg.chunk + 1];
+      src.lim = a.lim(sg.chunk);
       uint32_t dm = 0, nl = 0, csm = 0;
       const int len = (int)(sg.hi - sg.lo);
       for (int i = 0; i < len; ++i) {
@@ -317,7 +317,7 @@ DA_HDF void tile(const LibfmArgs &a, svm::Shared &sh, BK &bk, uint64_t k) {
         m &= m - 1;
         const uint64_t x = sg.lo + i;
         while (x >= a.cs[chunk + 1]) ++chunk;
-        src.lim = a.cs[chunk + 1];
+        src.lim = a.lim(chunk);
         const Head h = head_parse(src, x, a.cs[chunk + 1]);
         if (h.r1 != kNone) {
           if (h.r1 < wend) atomic_or_u32(&sh.r1bits[(h.r1 - w0) >> 5], 1u << ((h.r1 - w0) & 31));

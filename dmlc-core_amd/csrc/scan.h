@@ -60,5 +60,23 @@ __global__ void chunk_fixup_kernel(uint64_t *chunk_tab, int nchunk, const uint64
   }
 }
 
+// Before the exact write pass: when the gate handed the input over, forget the
+// chunk-table rows the single-pass kernel wrote (units the exact kernels never
+// visit -- no line in them -- then take the next unit's counts in
+// chunk_fixup_kernel instead of stale single-pass ones).
+__global__ void tab_reset_kernel(uint64_t *tab, uint64_t n, const uint32_t *gate) {
+  if (*gate == 0) return;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    tab[i] = ~0ull;
+}
+
+// The fill phase of a COUNT_ONLY -> FILL_ONLY pair reuses the tile bases of
+// the count phase.  When that count ran on the single-pass kernel (gate 0)
+// but the single-pass write kernel then hands over (the kSpinLimit valve sets
+// gate bit 1), no exact-path tile bases exist yet: the fill phase must count
+// first.  gate[1] = the gate as the count phase left it; gate[2] = "recount".
+__global__ void note_gate_kernel(uint32_t *gate) { gate[1] = gate[0]; }
+__global__ void recount_flag_kernel(uint32_t *gate) { gate[2] = (gate[0] != 0 && gate[1] == 0) ? 1u : 0u; }
+
 }  // namespace
 }  // namespace dmlc_amd

@@ -555,6 +555,9 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
 #else
     (void)rounds;
 #endif
+#ifdef DMLC_AMD_VALVE_TEST  // test-only build (lib/variants): the write pass of tile 1 hands over
+    if (MODE == 2 && k == 1 && tid == 0) atomic_or_u32(a.gate, 2u);
+#endif
   }
   bk.sync();
   FAST_STAMP(k, 5);

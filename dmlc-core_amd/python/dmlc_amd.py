@@ -29,7 +29,7 @@ class Params(ctypes.Structure):
                 ("value_type", ctypes.c_int32), ("indexing_mode", ctypes.c_int32),
                 ("label_column", ctypes.c_int32), ("weight_column", ctypes.c_int32),
                 ("delimiter", ctypes.c_int32), ("tile_bytes", ctypes.c_uint32),
-                ("flags", ctypes.c_uint32), ("reserved", ctypes.c_uint32 * 3)]
+                ("flags", ctypes.c_uint32), ("nthread", ctypes.c_int32), ("reserved", ctypes.c_uint32 * 2)]
 
 
 class Csr(ctypes.Structure):
@@ -97,7 +97,7 @@ EXPORTED_SYMBOLS = ("dmlc_amd_parse", "dmlc_amd_workspace_bytes", "dmlc_amd_erro
 
 
 def make_params(fmt="libsvm", index_bits=32, value_type="f32", indexing_mode=0, label_column=-1,
-                weight_column=-1, delimiter=",", tile_bytes=0, flags=0):
+                weight_column=-1, delimiter=",", tile_bytes=0, flags=0, nthread=1):
     p = Params()
     p.format = _FMT[fmt] if isinstance(fmt, str) else int(fmt)
     p.index_bits = index_bits
@@ -108,7 +108,13 @@ def make_params(fmt="libsvm", index_bits=32, value_type="f32", indexing_mode=0, 
     p.delimiter = ord(delimiter) if isinstance(delimiter, str) else int(delimiter)
     p.tile_bytes = tile_bytes
     p.flags = flags
+    p.nthread = nthread
     return p
+
+
+def units_per_chunk(params):
+    """ParseBlock units per chunk (FillData ranges, dmlc_amd_params.nthread)."""
+    return max(int(params.nthread), 1)
 
 
 def _torch():
@@ -221,7 +227,8 @@ class DeviceParser:
         counts = self.count(text, chunk_starts, stream, result=res)
         out = self.alloc(counts)
         nchunks = int(chunk_starts.numel()) - 1
-        out["chunk_table"] = torch.zeros(max(nchunks, 1) * 8, dtype=torch.int64, device="cuda")
+        nunits = nchunks * units_per_chunk(self.params)
+        out["chunk_table"] = torch.zeros(max(nunits, 1) * 8, dtype=torch.int64, device="cuda")
         self.fill_async(text, chunk_starts, out, res,
                         chunk_table=out["chunk_table"] if nchunks > 0 else None, stream=stream)
         r = res.cpu().numpy().view(np.uint64)
@@ -276,6 +283,7 @@ def parse_bytes(data, chunk_offsets=None, fmt="libsvm", exact=False, **kw):
     h["error"] = out["error"]
     h["path"] = "exact" if out["path"] else "fast"
     h["counts"] = out["counts"]
+    h["units_per_chunk"] = units_per_chunk(p.params)
     return h
 
 
@@ -302,7 +310,8 @@ def strtof_batch(strings):
 
 
 def chunk_check(h, fmt, nchunks, total_counts):
-    """Per-chunk consistency CHECKs of the reference, applied to GPU output.
+    """Per-unit consistency CHECKs of the reference, applied to GPU output
+    (nchunks: table rows, i.e. chunks x units per chunk).
 
     The reference raises these from RowBlockContainer::GetBlock (row_block.h:
     174-178) and, for CSV, from ParseBlock itself (csv_parser.h:147-148); libfm

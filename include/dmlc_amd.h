@@ -12,13 +12,18 @@
  *
  * Semantics: the text buffer holds `nchunks` consecutive InputSplit chunks
  * (chunk c = [chunk_starts[c], chunk_starts[c+1]), chunk_starts[nchunks] ==
- * nbytes).  Each chunk is parsed as ONE ParseBlock (the reference with
- * nthread = 1, text_parser.h:116-155) and the per-chunk RowBlockContainers are
- * returned concatenated, exactly as RowBlockContainer::Push(RowBlock)
- * (src/data/row_block.h:126-168) would concatenate them: offsets are global.
- * Per-chunk boundaries are reported in chunk_table so the caller can rebuild
- * the per-chunk RowBlock views (and run GetBlock's consistency CHECKs,
- * row_block.h:171-189, per chunk).
+ * nbytes).  Each chunk goes through TextParserBase::FillData
+ * (text_parser.h:116-155): it is cut into T = max(params.nthread, 1) ranges
+ * (BackFindEndLine, text_parser.h:70-77) and each range is parsed as ONE
+ * ParseBlock -- a "unit"; unit u = c * T + t.  The per-unit
+ * RowBlockContainers are returned concatenated, exactly as
+ * RowBlockContainer::Push(RowBlock) (src/data/row_block.h:126-168) would
+ * concatenate them: offsets are global.  Per-unit boundaries are reported in
+ * chunk_table so the caller can rebuild the per-unit RowBlock views (the
+ * reference's blocks, parser.h:32-48) and run GetBlock's consistency CHECKs
+ * (row_block.h:171-189) per unit.  T changes the result only through
+ * indexing_mode < 0, whose 1-based detection is per unit
+ * (libsvm_parser.h:165-171, libfm_parser.h likewise).
  *
  * All pointers named d_* and every pointer inside dmlc_amd_csr are DEVICE
  * pointers.  Calls are asynchronous on `stream` (a hipStream_t, NULL = default
@@ -36,7 +41,7 @@
 extern "C" {
 #endif
 
-#define DMLC_AMD_ABI_VERSION 1
+#define DMLC_AMD_ABI_VERSION 2
 
 enum { DMLC_AMD_LIBSVM = 0, DMLC_AMD_CSV = 1, DMLC_AMD_LIBFM = 2 };
 enum { DMLC_AMD_F32 = 0, DMLC_AMD_I32 = 1, DMLC_AMD_I64 = 2 };
@@ -74,7 +79,9 @@ typedef struct dmlc_amd_params {
   int32_t delimiter;     /* csv: CSVParserParam::delimiter[0] (csv_parser.h:37) */
   uint32_t tile_bytes;   /* 0 = default tile size */
   uint32_t flags;        /* DMLC_AMD_FLAG_* */
-  uint32_t reserved[3];
+  int32_t nthread;       /* FillData ranges per chunk (TextParserBase::nthread_, text_parser.h:32-35);
+                            0 or 1 = one ParseBlock per chunk */
+  uint32_t reserved[2];
 } dmlc_amd_params;
 
 #define DMLC_AMD_FLAG_COUNT_ONLY 1u /* run the counting passes only (size query) */
@@ -108,8 +115,9 @@ typedef struct dmlc_amd_result {
 /* Bytes of device workspace dmlc_amd_parse needs for this input. */
 size_t dmlc_amd_workspace_bytes(uint64_t nbytes, int nchunks, const dmlc_amd_params *prm);
 
-/* Parse.  d_chunk_table (optional, may be NULL) receives nchunks x 8 uint64:
- * the exclusive counts (slots above) at each chunk start.  Returns DMLC_AMD_OK
+/* Parse.  d_chunk_table (optional, may be NULL) receives (nchunks * T) x 8
+ * uint64, T = max(nthread, 1): the exclusive counts (slots above) at each
+ * unit start.  Returns DMLC_AMD_OK
  * or DMLC_AMD_ERR_ARG / DMLC_AMD_ERR_HIP; parse errors are reported through
  * d_result->error once the stream reaches the end of the pipeline. */
 int dmlc_amd_parse(const void *d_text, uint64_t nbytes, const uint64_t *d_chunk_starts, int nchunks,

@@ -126,6 +126,8 @@ def ref_lib():
                                     ctypes.POINTER(ctypes.c_double)]
         L.ref_split_chunks.argtypes = [ctypes.c_char_p, ctypes.c_uint, ctypes.c_uint,
                                        ctypes.POINTER(Chunks)]
+        L.ref_parse_chunks.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(Params),
+                                       ctypes.POINTER(Csr)]
         L.ref_parse_float.restype = ctypes.c_float
         L.ref_parse_float.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_size_t)]
         L.ref_bench_blocks.restype = ctypes.c_double
@@ -246,6 +248,32 @@ def ref_parse_block(data, **kw):
     oracle_lib().dmo_csr_init(ctypes.byref(c), prm.value_kind)
     ref_lib().ref_parse_block(ctypes.cast(buf, ctypes.c_void_p), len(raw), ctypes.byref(prm),
                               ctypes.byref(c))
+    out = _csr_to_dict(c, prm.value_kind, prm.index_bits)
+    oracle_lib().dmo_csr_free(ctypes.byref(c))
+    return out
+
+
+def ref_parse_chunks(data, chunk_offsets, **kw):
+    """Genuine reference: each chunk through TextParserBase::FillData with
+    ``nthread`` ranges (the ParseNext seam of oracle/ref_harness.cc); one
+    block per non-empty container.  DMLC_REF_NPROCS lifts the reference's
+    omp_get_num_procs()-based thread cap for this call."""
+    prm = params(**kw)
+    raw = _as_bytes(data)
+    buf = ctypes.create_string_buffer(raw, len(raw) + 1)
+    offs = np.ascontiguousarray(chunk_offsets, dtype=np.uint64)
+    c = Csr()
+    oracle_lib().dmo_csr_init(ctypes.byref(c), prm.value_kind)
+    old = os.environ.get("DMLC_REF_NPROCS")
+    os.environ["DMLC_REF_NPROCS"] = str(2 * max(prm.nthread, 1) + 8)
+    try:
+        ref_lib().ref_parse_chunks(ctypes.cast(buf, ctypes.c_void_p), offs.ctypes.data, len(offs) - 1,
+                                   ctypes.byref(prm), ctypes.byref(c))
+    finally:
+        if old is None:
+            del os.environ["DMLC_REF_NPROCS"]
+        else:
+            os.environ["DMLC_REF_NPROCS"] = old
     out = _csr_to_dict(c, prm.value_kind, prm.index_bits)
     oracle_lib().dmo_csr_free(ctypes.byref(c))
     return out

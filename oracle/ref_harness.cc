@@ -14,6 +14,8 @@
 #include <dmlc/io.h>
 #include <dmlc/strtonum.h>
 
+#include <dlfcn.h>
+
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -30,7 +32,45 @@
 
 using dmlc::data::RowBlockContainer;
 
+// TextParserBase caps its thread count at max(omp_get_num_procs() / 2 - 4, 1)
+// (text_parser.h:32-35): 1 in an 8-CPU build container, 2 on the 256-core GPU
+// host.  To run the genuine FillData range split with nthread > 1 here, this
+// test library answers omp_get_num_procs from DMLC_REF_NPROCS when that is set
+// (symbol interposition inside this .so), and forwards to libgomp otherwise.
+extern "C" int omp_get_num_procs(void) {
+  if (const char *e = std::getenv("DMLC_REF_NPROCS")) return std::atoi(e);
+  using Fn = int (*)(void);
+  static Fn real = reinterpret_cast<Fn>(dlsym(RTLD_NEXT, "omp_get_num_procs"));
+  return real ? real() : 1;
+}
+
 namespace {
+
+// An InputSplit over chunks already in memory (the ParseNext seam below).
+class MemSplit : public dmlc::InputSplit {
+ public:
+  MemSplit(const char *buf, const uint64_t *off, int n) : buf_(buf), off_(off), n_(n) {}
+  size_t GetTotalSize(void) override { return (size_t)off_[n_]; }
+  void BeforeFirst(void) override { i_ = 0; }
+  bool NextRecord(Blob *) override { return false; }
+  bool NextChunk(Blob *out) override {
+    if (i_ >= n_) return false;
+    // a private copy with a NUL after its end, like the InputSplit's own buffer
+    cur_.assign(buf_ + off_[i_], buf_ + off_[i_ + 1]);
+    cur_.push_back('\0');
+    out->dptr = &cur_[0];
+    out->size = (size_t)(off_[i_ + 1] - off_[i_]);
+    ++i_;
+    return true;
+  }
+  void ResetPartition(unsigned, unsigned) override { i_ = 0; }
+
+ private:
+  const char *buf_;
+  const uint64_t *off_;
+  int n_, i_ = 0;
+  std::vector<char> cur_;
+};
 
 template <typename I, typename D>
 struct SvmSeam : public dmlc::data::LibSVMParser<I, D> {
@@ -169,6 +209,18 @@ int block_sparse(const char *buf, size_t n, const dmo_params *p, dmo_csr *o) {
   return 0;
 }
 
+// FillData over each chunk with the parser's own nthread (the genuine range
+// split, text_parser.h:116-155); every non-empty container is one block, as
+// ParserImpl::Next hands them out (parser.h:32-48).
+template <class P, typename I, typename D>
+int chunks_typed(const char *buf, const uint64_t *off, int n, const dmo_params *p, dmo_csr *o) {
+  P parser(new MemSplit(buf, off, n), args_of(p), p->nthread > 0 ? p->nthread : 1);
+  std::vector<RowBlockContainer<I, D>> data;
+  while (parser.ParseNext(&data))
+    for (const auto &c : data) append_container(o, c);
+  return 0;
+}
+
 template <typename I, typename D>
 int uri_typed(const char *uri, unsigned part, unsigned nparts, const char *type, dmo_csr *o,
               double *seconds) {
@@ -208,6 +260,33 @@ int ref_parse_block(const char *buf, size_t n, const dmo_params *p, dmo_csr *o) 
         return i64 ? block_csv<uint64_t, int32_t>(buf, n, p, o) : block_csv<uint32_t, int32_t>(buf, n, p, o);
       default:
         return i64 ? block_csv<uint64_t, int64_t>(buf, n, p, o) : block_csv<uint32_t, int64_t>(buf, n, p, o);
+    }
+  });
+}
+
+// Chunks buf[off[i], off[i+1]) through TextParserBase::FillData with
+// p->nthread ranges each (set DMLC_REF_NPROCS >= 2 * nthread + 8 so the
+// reference's cap admits them).
+int ref_parse_chunks(const char *buf, const uint64_t *off, int n, const dmo_params *p, dmo_csr *o) {
+  using namespace dmlc::data;
+  return guarded(o, [&] {
+    const bool i64 = p->index_bits == 64;
+    if (p->format == DMO_FMT_LIBSVM)
+      return i64 ? chunks_typed<LibSVMParser<uint64_t, float>, uint64_t, float>(buf, off, n, p, o)
+                 : chunks_typed<LibSVMParser<uint32_t, float>, uint32_t, float>(buf, off, n, p, o);
+    if (p->format == DMO_FMT_LIBFM)
+      return i64 ? chunks_typed<LibFMParser<uint64_t, float>, uint64_t, float>(buf, off, n, p, o)
+                 : chunks_typed<LibFMParser<uint32_t, float>, uint32_t, float>(buf, off, n, p, o);
+    switch (p->value_kind) {
+      case DMO_VAL_F32:
+        return i64 ? chunks_typed<CSVParser<uint64_t, float>, uint64_t, float>(buf, off, n, p, o)
+                   : chunks_typed<CSVParser<uint32_t, float>, uint32_t, float>(buf, off, n, p, o);
+      case DMO_VAL_I32:
+        return i64 ? chunks_typed<CSVParser<uint64_t, int32_t>, uint64_t, int32_t>(buf, off, n, p, o)
+                   : chunks_typed<CSVParser<uint32_t, int32_t>, uint32_t, int32_t>(buf, off, n, p, o);
+      default:
+        return i64 ? chunks_typed<CSVParser<uint64_t, int64_t>, uint64_t, int64_t>(buf, off, n, p, o)
+                   : chunks_typed<CSVParser<uint32_t, int64_t>, uint32_t, int64_t>(buf, off, n, p, o);
     }
   });
 }

@@ -150,9 +150,34 @@ void chunk_fixup(uint64_t *tab, int nchunk, const uint64_t *res) {
 
 }  // namespace
 
-extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *cs, int nchunks,
+extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *ccs, int nchunks_in,
                          const dmlc_amd_params *prm, const dmlc_amd_csr *out, uint64_t *chunk_table,
                          uint64_t *res /* 16 */) {
+  // FillData ranges (nthread > 1) as ParseBlock units, as capi.cpp does with
+  // range_kernel (ranges.hip): BackFindEndLine, text_parser.h:70-77,116-155
+  const int upc = prm->nthread > 1 && nbytes > 0 ? prm->nthread : 1;
+  std::vector<uint64_t> unit_starts;
+  const uint64_t *cs = ccs;
+  int nchunks = nchunks_in;
+  if (upc > 1) {
+    for (int c = 0; c < nchunks_in; ++c) {
+      const uint64_t head = ccs[c], size = ccs[c + 1] - head, nstep = (size + upc - 1) / upc;
+      for (int t = 0; t < upc; ++t) {
+        const uint64_t sb = (uint64_t)t * nstep < size ? (uint64_t)t * nstep : size;
+        uint64_t p = head + sb, r = head;
+        for (; p > head; --p)
+          if (p < head + size && (text[p] == '\n' || text[p] == '\r')) {
+            r = p;
+            break;
+          }
+        unit_starts.push_back(t == 0 ? head : r);
+      }
+    }
+    unit_starts.push_back(nbytes);
+    cs = unit_starts.data();
+    nchunks = nchunks_in * upc;
+  }
+  const UnitLim ul{ccs, upc};
   const uint64_t T = prm->tile_bytes ? prm->tile_bytes : (256ull << 10);
   const uint64_t ntiles = (nbytes + T - 1) / T;
   const bool count_only = prm->flags & DMLC_AMD_FLAG_COUNT_ONLY;
@@ -180,6 +205,7 @@ extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *c
     a.n = nbytes;
     a.cs = cs;
     a.nchunk = nchunks;
+    a.ul = ul;
     a.tile_bytes = T;
     a.ntiles = (uint32_t)ntiles;
     a.wide = prm->index_bits == 64;
@@ -246,6 +272,7 @@ extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *c
       }
       tile_scan(tile_cnt, tile_base, ntiles, res);
       if (!count_only && out->offset && res[C_ROWS] < out->cap[C_ROWS] + 1) out->offset[res[C_ROWS]] = res[C_INDEX];
+      if (!count_only) chunk_prefill(chunk_table, nchunks);  // tab_reset_kernel (scan.h)
       if (!count_only)
         for (uint64_t k = 0; k < ntiles; ++k) {
           svm::Shared *sh = new svm::Shared;
@@ -267,6 +294,7 @@ extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *c
     a.n = nbytes;
     a.cs = cs;
     a.nchunk = nchunks;
+    a.ul = ul;
     a.tile_bytes = T;
     a.ntiles = (uint32_t)ntiles;
     a.wide = prm->index_bits == 64;
@@ -353,6 +381,7 @@ extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *c
     }
     tile_scan(tile_cnt, tile_base, ntiles, res);
     if (!count_only && out->offset && res[C_ROWS] < out->cap[C_ROWS] + 1) out->offset[res[C_ROWS]] = res[C_INDEX];
+    if (!count_only) chunk_prefill(chunk_table, nchunks);  // tab_reset_kernel (scan.h)
     if (!count_only)
       for (uint64_t k = 0; k < ntiles; ++k) {
         csv::Shared *sh = new csv::Shared;
@@ -403,6 +432,7 @@ int main(int argc, char **argv) {
   prm.weight_column = std::atoi(argv[6]);
   prm.delimiter = std::atoi(argv[7]);
   prm.tile_bytes = (uint32_t)std::atoi(argv[8]);
+  if (const char *nt = std::getenv("EMU_NTHREAD")) prm.nthread = std::atoi(nt);
   std::vector<char> text = slurp(argv[9]);
   std::vector<char> craw = slurp(argv[10]);
   std::vector<uint64_t> cs(craw.size() / 8);
@@ -424,7 +454,8 @@ int main(int argc, char **argv) {
        *index = std::malloc(res[1] * isz + 1), *field = std::malloc(res[6] * isz + 1);
   std::vector<float> weight(res[3] + 1);
   std::vector<uint64_t> qid(res[4] + 1);
-  std::vector<uint64_t> chunks((nch > 0 ? nch : 1) * 8, 0);
+  const int upc = prm.nthread > 1 && !text.empty() ? prm.nthread : 1;
+  std::vector<uint64_t> chunks((nch > 0 ? nch * upc : 1) * 8, 0);
   csr.offset = offset.data();
   csr.label = label;
   csr.weight = weight.data();

@@ -23,7 +23,7 @@ def build():
 
 
 def parse(data, chunk_offsets=None, fmt="libsvm", index_bits=32, value_type=0, indexing_mode=0,
-          label_column=-1, weight_column=-1, delimiter=",", tile_bytes=0, exact=False):
+          label_column=-1, weight_column=-1, delimiter=",", tile_bytes=0, exact=False, nthread=1):
     if not _BUILT:
         build()
     raw = data.encode("latin-1") if isinstance(data, str) else bytes(data)
@@ -37,6 +37,7 @@ def parse(data, chunk_offsets=None, fmt="libsvm", index_bits=32, value_type=0, i
         d = ord(delimiter) if isinstance(delimiter, str) else int(delimiter)
         env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=0:exitcode=77")
         env.pop("EMU_EXACT", None)
+        env["EMU_NTHREAD"] = str(int(nthread))
         if exact:
             env["EMU_EXACT"] = "1"
         r = subprocess.run([EXE, str(f), str(index_bits), str(int(value_type)), str(indexing_mode),

@@ -13,6 +13,10 @@ Outputs (data only -- inputs and the reference's outputs, no reference source):
                  Parser<uint32_t>::Create on a real file: per-array SHA-256 and
                  the first/last 64 rows in full.
   split.json     InputSplit("text") chunk sizes/hashes and multi-part row counts.
+  filldata.json  TextParserBase::FillData with nthread = 1..4 ranges per chunk
+                 (text_parser.h:116-155) over multi-chunk inputs: every array
+                 plus the per-block row/index/value counts the reference's
+                 ParserImpl::Next hands out (one block per non-empty range).
 """
 import hashlib
 import json
@@ -335,10 +339,97 @@ def gen_split():
     print("split.json:", len(res["cases"]), "cases")
 
 
+def _fd_text(rng, fmt):
+    alpha = {po.LIBSVM: list("0123456789") * 6 + list("  ::.-+eE#\t") + ["qid:", "\r", " 0:1", " 1:2"],
+             po.CSV: list("0123456789") * 6 + list(",,,,.-+eE \t") + ["nan", "\xef\xbb\xbf"],
+             po.LIBFM: list("0123456789") * 6 + list("  :::.-+eE#\t") + ["\r", " 0:0:1", " 1:1:1"]}[fmt]
+
+    def structured():
+        if fmt == po.CSV:
+            return ",".join("%.4g" % rng.random() if rng.random() < 0.9 else "" for _ in range(int(rng.integers(1, 8))))
+        toks = ["%d" % rng.integers(0, 2)]
+        if fmt == po.LIBSVM and rng.random() < 0.2:
+            toks.append("qid:%d" % rng.integers(0, 9))
+        for _ in range(int(rng.integers(0, 8))):
+            v = "%.3g" % rng.random()
+            i = int(rng.integers(0, 20))
+            toks.append("%d:%s" % (i, v) if fmt == po.LIBSVM else "%d:%d:%s" % (rng.integers(0, 4), i, v))
+        line = " ".join(toks)
+        if rng.random() < 0.15:
+            line += " # c"
+        return line
+
+    lines = []
+    for _ in range(int(rng.integers(1, 14))):
+        if rng.random() < 0.7:
+            lines.append(structured())
+        else:
+            lines.append("".join(alpha[int(i)] for i in rng.integers(0, len(alpha), int(rng.integers(0, 50)))))
+    return ("\n".join(lines) + "\n").encode("latin-1")
+
+
+def _fd_chunks(rng, data):
+    nl = [i + 1 for i, b in enumerate(data) if b in (10, 13) and i + 1 < len(data)]
+    k = int(rng.integers(0, min(4, len(nl)) + 1)) if nl else 0
+    cuts = sorted(set(rng.choice(nl, size=k, replace=False).tolist())) if k else []
+    return [0] + cuts + [len(data)]
+
+
+def gen_filldata():
+    """FillData range-split goldens (the reference's ParseNext with nthread
+    ranges per chunk; DMLC_REF_NPROCS lifts its omp_get_num_procs cap)."""
+    rng = np.random.default_rng(20261016)
+    L, C, F = po.LIBSVM, po.CSV, po.LIBFM
+    fixed = [
+        # min index per range decides the 1-based shift (libsvm_parser.h:165-171)
+        ("zero_in_first_half", L, b"1 0:1 2:3\n0 5:1\n1 1:2 7:1\n0 3:4\n", -1),
+        ("zero_in_second_half", L, b"1 1:1 2:3\n0 5:1\n1 0:2 7:1\n0 3:4\n", -1),
+        ("tiny_chunk_empty_ranges", L, b"1 1:1\n", -1),
+        ("qid_newline_at_cut", L, b"1 qid:\n7 3:1\n0 qid:\n9 2:2\n", 0),
+        ("comment_first_line", L, b"# head\n1 1:1\n0 2:2 # tail\n1 3:3\n", -1),
+        ("libfm_dangling_at_cut", F, b"1 1:2:3 4:\n5:6 7:8:9\n0 2:\n3:1:1\n", -1),
+        ("libfm_zero_field", F, b"1 0:1:1 2:2:2\n0 3:3:3\n1 1:1:1\n0 2:2:2\n", -1),
+        ("csv_blank_field_at_cut", C, b"1,2, \n\n3,4\n5, \n6,7\n", 0),
+    ]
+    out = []
+
+    def record(name, fmt, data, offs, nthread, kw):
+        kw = dict(kw, fmt=fmt, nthread=nthread)
+        r = po.ref_parse_chunks(data, offs, **kw)
+        rec = {"name": name, "data_latin1": data.decode("latin-1"), "offs": [int(x) for x in offs],
+               "params": kw, "status": int(r["status"] != 0), "msg": r["msg"]}
+        if r["status"] == 0:
+            rec["expect"] = {k: enc(r[k]) for k in ("offset", "label", "weight", "qid", "field",
+                                                      "index", "value")}
+            rec["blocks"] = {k: [int(x) for x in r["blocks"][k]] for k in ("rows", "index", "value")}
+        out.append(rec)
+
+    for name, fmt, data, im in fixed:
+        for nt in (1, 2, 3, 4):
+            kw = {} if fmt == C else {"indexing_mode": im}
+            record("%s_t%d" % (name, nt), fmt, data, [0, len(data)], nt, kw)
+    for it in range(150):
+        fmt = (L, C, F)[it % 3]
+        data = _fd_text(rng, fmt)
+        offs = _fd_chunks(rng, data)
+        kw = {}
+        if fmt != C:
+            kw["indexing_mode"] = int(rng.integers(-1, 2))
+            if rng.random() < 0.2:
+                kw["index_bits"] = 64
+        elif rng.random() < 0.3:
+            kw["label_column"] = int(rng.integers(0, 2))
+        record("fuzz%03d" % it, fmt, data, offs, int(rng.integers(1, 5)), kw)
+    with open(os.path.join(OUT, "filldata.json"), "w") as f:
+        json.dump(out, f, indent=0)
+    print("filldata.json:", len(out), "cases,", sum(r["status"] for r in out), "error cases")
+
+
 if __name__ == "__main__":
     if not po.ref_available():
         sys.exit("build the reference first: make -C oracle ref")
-    gen_cases()
-    gen_floats()
-    gen_synth()
-    gen_split()
+    only = sys.argv[1:]
+    for name, fn in (("cases", gen_cases), ("floats", gen_floats), ("synth", gen_synth), ("split", gen_split),
+                     ("filldata", gen_filldata)):
+        if not only or name in only:
+            fn()

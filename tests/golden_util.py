@@ -45,3 +45,15 @@ FIELDS = ("offset", "label", "weight", "qid", "field", "index", "value")
 def diff(got, exp):
     """Return list of field names that differ."""
     return [k for k in FIELDS if k in exp and not same(got[k], exp[k])]
+
+
+def blocks_of(h):
+    """Per-block (rows, index, value) counts of a GPU / emulator result, from
+    its per-unit table (one row per ParseBlock unit, dmlc_amd.h chunk_table):
+    the blocks the reference's ParserImpl::Next hands out are the units with
+    at least one row (parser.h:32-48)."""
+    tab = np.asarray(h["chunk_table"], dtype=np.int64).reshape(-1, 8)
+    tot = np.asarray(h["counts"][:8], dtype=np.int64)[None, :]
+    per = np.vstack([tab[1:], tot]) - tab
+    keep = per[:, 0] > 0
+    return {"rows": per[keep, 0].tolist(), "index": per[keep, 1].tolist(), "value": per[keep, 2].tolist()}

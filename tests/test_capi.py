@@ -41,7 +41,7 @@ def test_python_binding_lists_every_export():
 
 def test_abi_version_and_error_strings(lib):
     lib.dmlc_amd_abi_version.restype = ctypes.c_int
-    assert lib.dmlc_amd_abi_version() == 1
+    assert lib.dmlc_amd_abi_version() == 2
     lib.dmlc_amd_error_string.restype = ctypes.c_char_p
     assert b"sign == true" in lib.dmlc_amd_error_string(1)
     assert b"NAN" in lib.dmlc_amd_error_string(2)

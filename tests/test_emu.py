@@ -7,7 +7,7 @@ import numpy as np
 import pytest
 
 import fuzz_text
-from golden_util import dec, diff, load_cases
+from golden_util import blocks_of, dec, diff, load_cases, load_json
 from oracle import pyoracle as po
 from tests.emu import pyemu
 from tools import synth
@@ -254,3 +254,24 @@ def test_emu_libfm_fast_vs_oracle():
         if it % 3 != 2 and it % 5 != 4:
             assert h["path"] == "fast", (it, data[:300])
     assert paths["fast"] >= 15 and paths["exact"] >= 3, paths
+
+
+FILLDATA = load_json("filldata.json")
+
+
+@pytest.mark.parametrize("case", FILLDATA[::3], ids=[c["name"] for c in FILLDATA[::3]])
+def test_emu_filldata_goldens(case):
+    """FillData ranges as ParseBlock units (host-computed in the emulator,
+    range_kernel on the GPU): the reference's arrays, errors and blocks."""
+    prm = case["params"]
+    data = case["data_latin1"].encode("latin-1")
+    offs = case["offs"]
+    h = pyemu.parse(data, offs, FMT[prm["fmt"]], nthread=prm.get("nthread", 1), **kw_of(prm))
+    nunits = (len(offs) - 1) * max(prm.get("nthread", 1), 1)
+    failed = check_fail(h, FMT[prm["fmt"]], [0] * (nunits + 1))
+    assert failed == bool(case["status"]), (h["error"], case["msg"])
+    if case["status"]:
+        return
+    exp = {k: dec(v) for k, v in case["expect"].items()}
+    assert diff(h, exp) == []
+    assert blocks_of(h) == case["blocks"]

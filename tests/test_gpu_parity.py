@@ -9,7 +9,7 @@ import hashlib
 import numpy as np
 import pytest
 
-from golden_util import FIELDS, dec, diff, load_cases, load_floats, load_json, same
+from golden_util import FIELDS, blocks_of, dec, diff, load_cases, load_floats, load_json, same
 from oracle import pyoracle as po
 from tools import synth
 
@@ -34,8 +34,6 @@ def gpu_kwargs(params):
             continue
         if k == "value_kind":
             kw["value_type"] = int(v)
-        elif k == "nthread":
-            continue
         else:
             kw[k] = v
     return kw
@@ -45,6 +43,7 @@ def gpu_parse(dm, data, chunk_offsets=None, fmt=po.LIBSVM, **kw):
     name = FMT_NAME[fmt]
     h = dm.parse_bytes(data, chunk_offsets, fmt=name, **kw)
     nch = (len(chunk_offsets) - 1) if chunk_offsets is not None else (1 if len(data) else 0)
+    nch *= h["units_per_chunk"]
     failed = nch > 0 and dm.chunk_check(h, name, nch, h["counts"]) >= 0
     h["failed"] = bool(h["error"]) or failed
     return h
@@ -463,3 +462,73 @@ def test_gpu_libfm_fast_fuzz_vs_oracle(dm):
         if it % 3 != 2 and it % 5 != 4:
             assert h["path"] == "fast", it
     assert paths["fast"] >= 90 and paths["exact"] >= 30, paths
+
+
+# ------------------------------------------ FillData nthread range split --
+FILLDATA = load_json("filldata.json")
+
+
+def test_gpu_filldata_goldens(dm):
+    """TextParserBase::FillData with nthread = 1..4 ranges per chunk
+    (range_kernel + per-unit parsing): the genuine reference's arrays, errors
+    and per-block counts (indexing_mode < 0 detection is per range)."""
+    for case in FILLDATA:
+        prm = case["params"]
+        h = gpu_parse(dm, case["data_latin1"], case["offs"], prm["fmt"], **gpu_kwargs(prm))
+        assert h["failed"] == bool(case["status"]), (case["name"], h["error"], case["msg"])
+        if case["status"]:
+            continue
+        exp = {k: dec(v) for k, v in case["expect"].items()}
+        assert diff(h, exp) == [], case["name"]
+        assert blocks_of(h) == case["blocks"], case["name"]
+
+
+@pytest.mark.parametrize("fmt", [po.LIBSVM, po.CSV, po.LIBFM])
+def test_gpu_filldata_fuzz_vs_oracle(dm, fmt):
+    """nthread in {1, 2, 3} x indexing_mode in {-1, 0, 1} on the fast and the
+    exact path, many chunks and long lines: equal to the oracle's FillData."""
+    rng = np.random.default_rng(606 + fmt)
+    for it in range(90):
+        nthread = 1 + it % 3
+        if fmt == po.CSV:
+            data = fuzz_text.uniform_csv(rng, int(rng.integers(1, 300)), int(rng.integers(1, 30)), ",",
+                                         violate=it % 5 == 4)
+            kw = {}
+        elif fmt == po.LIBSVM:
+            data = fuzz_text.uniform_libsvm(rng, int(rng.integers(1, 300)), int(rng.integers(0, 30)),
+                                            violate=it % 5 == 4)
+            kw = {"indexing_mode": (it // 3) % 3 - 1}
+        else:
+            data = fuzz_text.uniform_libfm(rng, int(rng.integers(1, 300)), 10, violate=it % 5 == 4)
+            kw = {"indexing_mode": (it // 3) % 3 - 1}
+        offs = fuzz_text.random_cuts(rng, data, 6)
+        o = po.parse_chunks(data, offs, fmt=fmt, nthread=nthread, **kw)
+        for exact in (False, True):
+            h = gpu_parse(dm, data, offs, fmt, nthread=nthread, exact=exact, **kw)
+            assert (o["status"] != 0) == h["failed"], (it, exact, o["msg"], h["error"])
+            if o["status"] == 0:
+                assert diff(h, o) == [], (it, exact, kw, nthread)
+                assert blocks_of(h)["rows"] == o["blocks"]["rows"].tolist(), (it, exact)
+
+
+def test_gpu_valve_hand_over_vs_oracle(dm):
+    """a COUNT_ONLY that stood on the single-pass kernel followed by
+    a FILL_ONLY whose single-pass write hands over (the kSpinLimit valve) must
+    count on the exact path before writing.  The valve build makes tile 1 of
+    every write pass hand over; results must equal the oracle (child process:
+    the valve library replaces the product library)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lib = os.path.join(root, "dmlc-core_amd", "lib", "variants", "libdmlc_amd_valve.so")
+    assert os.path.exists(lib), "build it: make -C dmlc-core_amd valve"
+    r = subprocess.run([sys.executable, os.path.join(root, "tests", "valve_child.py")], capture_output=True,
+                       timeout=240)
+    assert r.returncode == 0, r.stderr.decode()[-3000:]
+    res = json.loads(r.stdout.decode().strip().splitlines()[-1])
+    for e in res:
+        assert e["split_path"] & 2 and e["full_path"] & 2, e  # the valve fired in the write pass
+        assert e["split_error"] == 0 and e["full_error"] == 0, e
+        assert e["split_diff"] == [] and e["full_diff"] == [], e

@@ -119,3 +119,43 @@ def test_oracle_fuzz_vs_reference(fmt):
         assert (r["status"] != 0) == (o["status"] != 0), (text, r["msg"], o["msg"])
         if r["status"] == 0:
             assert diff(o, r) == [], repr(text)
+
+
+# ---- FillData's nthread range split (text_parser.h:116-155) ----
+
+FILLDATA = load_json("filldata.json")
+
+
+@pytest.mark.parametrize("case", FILLDATA, ids=[c["name"] for c in FILLDATA])
+def test_oracle_filldata_goldens(case):
+    """The oracle's range split (dmo_parse_chunk with nthread) against the
+    genuine reference's ParseNext: arrays, errors and per-block counts."""
+    got = po.parse_chunks(case["data_latin1"], case["offs"], **case["params"])
+    assert (got["status"] != 0) == bool(case["status"]), (got["msg"], case["msg"])
+    if case["status"]:
+        return
+    exp = {k: dec(v) for k, v in case["expect"].items()}
+    assert diff(got, exp) == []
+    for k in ("rows", "index", "value"):
+        assert got["blocks"][k].tolist() == case["blocks"][k], k
+
+
+@pytest.mark.skipif(not po.ref_available(), reason="oracle/_ref not built (needs /root/reference)")
+@pytest.mark.parametrize("fmt", [po.LIBSVM, po.CSV, po.LIBFM])
+def test_oracle_filldata_fuzz_vs_reference(fmt):
+    """Live: oracle == reference ParseNext for nthread 2..4 on multi-chunk input."""
+    rng = np.random.default_rng(77 + fmt)
+    for it in range(150):
+        text = ("\n".join(_fuzz_line(rng, fmt) for _ in range(int(rng.integers(1, 9)))) + "\n").encode("latin-1")
+        nl = [i + 1 for i, b in enumerate(text) if b == 10 and i + 1 < len(text)]
+        cuts = sorted(set(rng.choice(nl, size=min(len(nl), int(rng.integers(0, 3))), replace=False).tolist())) if nl else []
+        offs = [0] + cuts + [len(text)]
+        kw = {"fmt": fmt, "nthread": int(rng.integers(2, 5))}
+        if fmt != po.CSV:
+            kw["indexing_mode"] = int(rng.integers(-1, 2))
+        r = po.ref_parse_chunks(text, offs, **kw)
+        o = po.parse_chunks(text, offs, **kw)
+        assert (r["status"] != 0) == (o["status"] != 0), (text, kw, r["msg"], o["msg"])
+        if r["status"] == 0:
+            assert diff(o, r) == [], (text, kw)
+            assert o["blocks"]["rows"].tolist() == r["blocks"]["rows"].tolist()
