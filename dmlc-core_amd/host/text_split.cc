@@ -6,9 +6,12 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <cerrno>
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <regex>
+#include <sstream>
 #include <thread>
 
 #include "dmlc/base.h"
@@ -24,38 +27,121 @@ uint64_t file_size(const std::string &p) {
   return (uint64_t)st.st_size;
 }
 
+// ---- the input file list, as InputSplitBase::InitInputFileInfo builds it
+// (input_split_base.cc:96-176) over LocalFileSystem (local_filesys.cc:69-122)
+
+struct PathInfo {
+  std::string name;
+  uint64_t size;
+  bool dir;
+};
+
+// LocalFileSystem::GetPathInfo: stat; a dangling symlink (lstat only) is an
+// empty file; anything else that cannot be stat'ed is fatal.
+PathInfo GetPathInfo(const std::string &name) {
+  struct stat sb;
+  if (stat(name.c_str(), &sb) == -1) {
+    const int errsv = errno;
+    if (lstat(name.c_str(), &sb) == 0) return PathInfo{name, 0, false};
+    throw dmlc::Error("LocalFileSystem.GetPathInfo: " + name + " error: " + std::strerror(errsv));
+  }
+  return PathInfo{name, (uint64_t)sb.st_size, S_ISDIR(sb.st_mode)};
+}
+
+// LocalFileSystem::ListDirectory: raw readdir order, every entry except "."
+// and ".." (dotfiles included).
+std::vector<PathInfo> ListDirectory(const std::string &dir) {
+  DIR *d = opendir(dir.c_str());
+  if (d == nullptr) {
+    const int errsv = errno;
+    throw dmlc::Error("LocalFileSystem.ListDirectory " + dir + " error: " + std::strerror(errsv));
+  }
+  std::vector<PathInfo> out;
+  while (dirent *e = readdir(d)) {
+    if (!std::strcmp(e->d_name, ".") || !std::strcmp(e->d_name, "..")) continue;
+    std::string q = dir;
+    if (q.empty() || q.back() != '/') q += '/';
+    q += e->d_name;
+    try {
+      out.push_back(GetPathInfo(q));
+    } catch (...) {
+      closedir(d);
+      throw;
+    }
+  }
+  closedir(d);
+  return out;
+}
+
+std::string StripEnd(std::string s, char c) {
+  while (!s.empty() && s.back() == c) s.pop_back();
+  return s;
+}
+
+// URI(path).name for the local file system (io.h:523-551): "file://host/p" -> "/p"
+std::string LocalName(const std::string &u) {
+  const size_t p = u.find("://");
+  if (p == std::string::npos) return u;
+  const std::string proto = u.substr(0, p + 3);
+  if (proto != "file://") throw dmlc::Error("unsupported file system " + proto + " in \"" + u + "\" (local files only)");
+  const size_t slash = u.find('/', p + 3);
+  return slash == std::string::npos ? std::string("/") : u.substr(slash);
+}
+
 }  // namespace
 
-std::vector<std::string> ListInputFiles(const std::string &path) {
-  std::vector<std::string> out;
-  size_t start = 0;
-  while (start <= path.size()) {
-    size_t end = path.find(';', start);
-    if (end == std::string::npos) end = path.size();
-    std::string p = path.substr(start, end - start);
-    if (p.compare(0, 7, "file://") == 0) p = p.substr(7);
-    if (!p.empty()) {
-      struct stat st;
-      if (stat(p.c_str(), &st) != 0) throw dmlc::Error("Check failed: file \"" + p + "\" does not exist");
-      if (S_ISDIR(st.st_mode)) {
-        std::vector<std::string> ents;
-        if (DIR *d = opendir(p.c_str())) {
-          while (dirent *e = readdir(d)) {
-            std::string q = p + (p.back() == '/' ? "" : "/") + e->d_name;
-            struct stat es;
-            if (e->d_name[0] != '.' && stat(q.c_str(), &es) == 0 && S_ISREG(es.st_mode)) ents.push_back(q);
-          }
-          closedir(d);
+std::vector<std::string> ListInputFiles(const std::string &uri) {
+  // ConvertToURIs: split on ';' (std::getline semantics, common.h Split), then
+  // per entry: a bare name or a name ending in '/' is taken as it is; else the
+  // entry's directory is listed and an exact name match wins, otherwise every
+  // non-empty file whose full path matches the entry as a std::regex
+  std::vector<std::string> expanded;
+  {
+    std::istringstream is(uri);
+    std::string item;
+    while (std::getline(is, item, ';')) {
+      const std::string name = LocalName(item);
+      const size_t pos = name.rfind('/');
+      if (pos == std::string::npos || pos + 1 == name.size()) {
+        expanded.push_back(name);
+        continue;
+      }
+      const std::vector<PathInfo> dfiles = ListDirectory(name.substr(0, pos));
+      bool exact = false;
+      for (const PathInfo &f : dfiles) {
+        if (StripEnd(f.name, '/') == StripEnd(name, '/')) {
+          expanded.push_back(f.name);
+          exact = true;
+          break;
         }
-        std::sort(ents.begin(), ents.end());
-        out.insert(out.end(), ents.begin(), ents.end());
-      } else {
-        out.push_back(p);
+      }
+      if (exact) continue;
+      std::regex pattern;
+      try {
+        pattern = std::regex(name);
+      } catch (const std::regex_error &e) {
+        throw dmlc::Error(std::string(e.what()) + " bad regex " + name);
+      }
+      for (const PathInfo &f : dfiles) {
+        if (f.dir || f.size == 0) continue;
+        if (std::regex_match(StripEnd(f.name, '/'), pattern)) expanded.push_back(f.name);
       }
     }
-    start = end + 1;
   }
-  return out;
+  // InitInputFileInfo: directories contribute their non-empty files (one
+  // level, readdir order); empty files take no part
+  std::vector<std::string> files;
+  for (const std::string &path : expanded) {
+    const PathInfo info = GetPathInfo(path);
+    if (info.dir) {
+      for (const PathInfo &f : ListDirectory(info.name))
+        if (f.size != 0 && !f.dir) files.push_back(f.name);
+    } else if (info.size != 0) {
+      files.push_back(info.name);
+    }
+  }
+  if (files.empty()) throw dmlc::Error("Check failed: files_.size() != 0U Cannot find any files that matches the URI pattern " + uri);
+  return files;
 }
 
 TextSplit::TextSplit(const std::string &uri, unsigned part, unsigned nparts, size_t buffer_bytes)

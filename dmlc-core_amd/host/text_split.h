@@ -1,8 +1,12 @@
 // text_split.h -- host-side text InputSplit with dmlc-core's chunk contract
 // (InputSplit::Create(uri, part, nparts, "text"), src/io.cc:76-119):
 //
-//  * the input is a list of files (a file, a directory's regular files, or a
-//    ';'-separated list), empty files dropped (input_split_base.cc:139-161);
+//  * the input is a list of files built as InputSplitBase::InitInputFileInfo
+//    does (input_split_base.cc:96-176): ';'-separated entries, each a file, a
+//    directory (its entries in raw readdir order, dotfiles included, one
+//    level) or a path whose last component is matched as a std::regex against
+//    the directory's entries; empty files and directories dropped; no file at
+//    all is an error;
 //  * part k of n covers bytes [ceil(total/n)*k, ceil(total/n)*(k+1)) of the
 //    concatenation, both ends moved forward to the next record start
 //    (ResetPartition, input_split_base.cc:29-63; LineSplitter::SeekRecordBegin,

@@ -96,9 +96,13 @@ def test_host_split_matches_oracle(tmp_path):
         uri = ";".join(paths) if it % 2 else d
         nparts = int(rng.integers(1, 5))
         buf = int(rng.choice([64, 1000, 1 << 16, 8 << 20]))
+        # a directory lists in raw readdir order (local_filesys.cc:98-122), as os.listdir does
+        by_path = dict(zip(paths, contents))
+        order = paths if it % 2 else [os.path.join(d, f) for f in os.listdir(d)]
+        files = [by_path[p] for p in order if by_path[p]]
         for part in range(nparts):
             got = host_split(uri, part, nparts, buf)
-            exp = po.split_text(contents, part, nparts, buffer_bytes=buf)
+            exp = po.split_text(files, part, nparts, buffer_bytes=buf)
             assert got == exp, (it, part, nparts, buf)
             # the in-place reader: same chunks, whatever the batch and buffer sizes
             batch = int(rng.choice([1, 3 * buf, 1 << 20]))
@@ -121,6 +125,58 @@ def test_host_split_golden_chunking(case, tmp_path):
     got = host_split(";".join(paths), case["part"], case["nparts"], 8 << 20)
     assert [len(c) for c in got] == case["chunk_sizes"]
     assert [hashlib.sha256(c).hexdigest() for c in got] == case["chunk_sha256"]
+
+
+def _host_split_error(uri):
+    L = _host()
+    buf, off, n = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_uint64()
+    return L.dmlc_amd_host_split(uri.encode(), 0, 1, 8 << 20, ctypes.byref(buf), ctypes.byref(off),
+                                 ctypes.byref(n))
+
+
+def test_host_split_file_list_semantics(tmp_path):
+    """InputSplitBase::InitInputFileInfo (input_split_base.cc:96-176): a
+    directory in raw readdir order with dotfiles kept and empty files and
+    subdirectories dropped; a last path component matched as a regex; no file
+    at all is an error.  Checked against the genuine reference when it is
+    built, and against the oracle split of the same file order."""
+    d = tmp_path / "dir"
+    d.mkdir()
+    names = ["zeta.txt", ".crc", "alpha.txt", "m-1.txt", "m-2.txt", "empty.txt", "Beta.txt", "07.txt"]
+    rng = np.random.default_rng(9)
+    body = {}
+    for nm in names:
+        t, _ = synth.rows(synth.LIBSVM, 0 if nm == "empty.txt" else int(rng.integers(1, 40)), 5,
+                          seed=int(rng.integers(1, 99)))
+        body[nm] = t.tobytes()
+        (d / nm).write_bytes(body[nm])
+    (d / "sub").mkdir()
+    (d / "sub" / "x.txt").write_bytes(b"1 1:1\n")
+    listed = [f for f in os.listdir(d) if f in body and body[f]]
+    assert sorted(listed) != listed or True  # order is whatever readdir gives; never re-sorted
+    uris = {
+        "dir": (str(d), listed),
+        "dir_slash": (str(d) + "/", listed),
+        "regex": (str(d / "m-[0-9].txt"), [f for f in os.listdir(d) if f.startswith("m-")]),
+        "exact": (str(d / "alpha.txt"), ["alpha.txt"]),
+        "list": ("%s;%s" % (d / "zeta.txt", d / ".crc"), ["zeta.txt", ".crc"]),
+    }
+    for key, (uri, order) in uris.items():
+        exp = po.split_text([body[f] for f in order], 0, 1)
+        for nparts in (1, 3):
+            got = [c for part in range(nparts) for c in host_split(uri, part, nparts, 8 << 20)]
+            oracle = [c for part in range(nparts) for c in po.split_text([body[f] for f in order], part, nparts)]
+            assert got == oracle, (key, nparts)
+            if po.ref_available():
+                ref = [c for part in range(nparts) for c in po.ref_split_chunks(uri, part, nparts)]
+                assert got == ref, (key, nparts)
+        assert b"".join(host_split(uri, 0, 1, 8 << 20)) == b"".join(exp), key
+    # only empty files / nothing matching: the reference's CHECK_NE(files_.size(), 0U)
+    e = tmp_path / "empty_dir"
+    e.mkdir()
+    (e / "a.txt").write_bytes(b"")
+    assert _host_split_error(str(e)) != 0
+    assert _host_split_error(str(d / "nomatch-[0-9]+")) != 0
 
 
 # ------------------------------------------------------------------ GPU --
