@@ -347,6 +347,13 @@ int dmlc_amd_parse(const void *d_text, uint64_t nbytes, const uint64_t *d_chunk_
     const bool use_fast = nbytes > 0 && prm->indexing_mode >= 0 && !(prm->flags & DMLC_AMD_FLAG_EXACT);
     e = dmlc_amd::launch_libfm(a, f, use_fast, res, phase, s);
   }
+  if (e == hipSuccess && (prm->flags & DMLC_AMD_FLAG_MAX_INDEX) && phase != dmlc_amd::kPhaseCount) {
+    // NumCol of the reference's BasicRowIter: maxima of what was written
+    const int wide = prm->index_bits == 64;
+    e = dmlc_amd::launch_max(out->index, wide, res + DMLC_AMD_INDEX, out->cap[DMLC_AMD_INDEX], res + 10, s);
+    if (e == hipSuccess)
+      e = dmlc_amd::launch_max(out->field, wide, res + DMLC_AMD_FIELD, out->cap[DMLC_AMD_FIELD], res + 11, s);
+  }
   g_last_hip = e;
   return e == hipSuccess ? DMLC_AMD_OK : DMLC_AMD_ERR_HIP;
 }

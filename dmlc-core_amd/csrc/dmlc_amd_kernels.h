@@ -29,6 +29,9 @@ hipError_t launch_libfm(const LibfmArgs &a, const FastSvmArgs &f, bool use_fast,
 // (text_parser.h:116-155); units[nchunk * nthread] = n.
 hipError_t launch_ranges(const uint8_t *text, const uint64_t *cs, int nchunk, int nthread, uint64_t n,
                          uint64_t *units, hipStream_t s);
+// *out = max(arr[0 .. min(*count, cap))) (0 when empty); arr is u32, or u64 when wide
+hipError_t launch_max(const void *arr, int wide, const uint64_t *count, uint64_t cap, uint64_t *out,
+                      hipStream_t s);
 hipError_t launch_csv(const CsvArgs &a, const FastCsvArgs &f, bool use_fast, uint64_t *res, int phase,
                       hipStream_t s);
 

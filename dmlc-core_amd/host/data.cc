@@ -1,0 +1,277 @@
+// data.cc -- this build's src/data.cc: the parser registry, the registered
+// HIP text parsers and the Parser / RowBlockIter factories.
+//
+//   Parser<I,D>::Create(uri, part, nparts, type)     src/data.cc:152-186
+//     CreateParser_: URISpec (uri?args#cache),
+//     "auto" -> format= or libsvm, registry lookup     src/data.cc:66-86
+//   RowBlockIter<I,D>::Create -> BasicRowIter         src/data.cc:88-150
+//   registrations: libsvm / libfm (real_t), csv
+//     (real_t / int32_t / int64_t) x (u32 / u64)      src/data.cc:189-227
+//
+// The registered factories build HipTextParser (hip_engine.h) over this
+// build's text InputSplit, read in place into pinned batches
+// (TextSplit::FillChunks).  Programs may register more parser types with
+// DMLC_REGISTER_DATA_PARSER; Create finds them by name the same way.
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "dmlc/data.h"
+#include "dmlc/logging.h"
+#include "dmlc/registry.h"
+#include "hip_engine.h"
+#include "text_split.h"
+
+namespace dmlc_amd {
+namespace {
+
+// io::URISpec (src/io/uri_spec.h:43-74): path?k=v&k2=v2#cachefile
+struct UriSpec {
+  std::string uri, cache_file;
+  std::map<std::string, std::string> args;
+  UriSpec(const std::string &full, unsigned part, unsigned nparts) {
+    auto split = [](const std::string &s, char d) {
+      std::vector<std::string> out;
+      std::istringstream is(s);
+      std::string item;
+      while (std::getline(is, item, d)) out.push_back(item);
+      return out;
+    };
+    const std::vector<std::string> name_cache = split(full, '#');
+    if (name_cache.size() == 2) {
+      std::ostringstream os;
+      os << name_cache[1];
+      if (nparts != 1) os << ".split" << nparts << ".part" << part;
+      cache_file = os.str();
+    } else {
+      CHECK_EQ(name_cache.size(), 1U) << "only one `#` is allowed in file path for cachefile specification";
+    }
+    const std::vector<std::string> name_args = split(name_cache.empty() ? std::string() : name_cache[0], '?');
+    if (name_args.size() == 2) {
+      const std::vector<std::string> arg_list = split(name_args[1], '&');
+      for (size_t i = 0; i < arg_list.size(); ++i) {
+        std::istringstream is(arg_list[i]);
+        std::pair<std::string, std::string> kv;
+        CHECK(std::getline(is, kv.first, '=')) << "Invalid uri argument format for key in arg " << i + 1;
+        CHECK(std::getline(is, kv.second)) << "Invalid uri argument format for value in arg " << i + 1;
+        args.insert(kv);
+      }
+    } else {
+      CHECK_EQ(name_args.size(), 1U) << "only one `#` is allowed in file path for cachefile specification";
+    }
+    uri = name_args.empty() ? std::string() : name_args[0];
+  }
+};
+
+// Chunks of this build's InputSplit read straight into the batch (no copy).
+class TextSplitSource : public ChunkSource {
+ public:
+  explicit TextSplitSource(TextSplit *s) : split_(s) {}
+  Fill FillChunks(char *dst, size_t cap, size_t max_bytes, std::vector<uint64_t> *ends) override {
+    const TextSplit::Fill f = split_->FillChunks(dst, cap, max_bytes, ends);
+    return Fill{f.end, f.need};
+  }
+  void BeforeFirst() override { split_->BeforeFirst(); }
+
+ private:
+  std::unique_ptr<TextSplit> split_;
+};
+
+// Set by RowBlockIter::Create around its parser's construction: the parser
+// then also reduces the index / field maxima on the device (NumCol).
+thread_local bool g_want_max_index = false;
+
+// The factory behind every registered text type: `format` is the name it
+// is registered under.  nthread follows TextParserBase (text_parser.h:32-35).
+template <typename I, typename D>
+dmlc::Parser<I, D> *CreateHipParser(const std::string &format, const std::string &path,
+                                    const std::map<std::string, std::string> &args, unsigned part,
+                                    unsigned nparts) {
+  EngineConfig cfg;
+  cfg.prm = make_params<I, D>(format, args);
+  cfg.prm.nthread = reference_nthread();
+  cfg.max_index = g_want_max_index;
+  cfg.from_env();
+  return new HipTextParser<I, D>(new TextSplitSource(new TextSplit(path, part, nparts)), cfg);
+}
+
+template <typename I, typename D>
+dmlc::Parser<I, D> *CreateLibSVMParser(const std::string &path, const std::map<std::string, std::string> &args,
+                                       unsigned part, unsigned nparts) {
+  return CreateHipParser<I, D>("libsvm", path, args, part, nparts);
+}
+template <typename I, typename D>
+dmlc::Parser<I, D> *CreateLibFMParser(const std::string &path, const std::map<std::string, std::string> &args,
+                                      unsigned part, unsigned nparts) {
+  return CreateHipParser<I, D>("libfm", path, args, part, nparts);
+}
+template <typename I, typename D>
+dmlc::Parser<I, D> *CreateCSVParser(const std::string &path, const std::map<std::string, std::string> &args,
+                                    unsigned part, unsigned nparts) {
+  return CreateHipParser<I, D>("csv", path, args, part, nparts);
+}
+
+template <typename I, typename D>
+dmlc::Parser<I, D> *CreateParser_(const char *uri, unsigned part, unsigned nparts, const char *type) {
+  std::string ptype = type ? type : "auto";
+  UriSpec spec(uri, part, nparts);
+  if (ptype == "auto") {
+    auto it = spec.args.find("format");
+    ptype = it == spec.args.end() ? std::string("libsvm") : it->second;
+  }
+  const dmlc::ParserFactoryReg<I, D> *e = dmlc::Registry<dmlc::ParserFactoryReg<I, D>>::Get()->Find(ptype);
+  if (e == nullptr) LOG(FATAL) << "Unknown data type " << ptype;
+  return (*e->body)(spec.uri, spec.args, part, nparts);
+}
+
+// BasicRowIter (src/data/basic_row_iter.h:24-79): every block of the parser
+// concatenated as RowBlockContainer::Push does (row_block.h:126-168);
+// NumCol = max_index + 1.  For this build's own parser the block counts and
+// the index / field maxima come from the device (DMLC_AMD_FLAG_MAX_INDEX), so
+// the copy is the only host pass over the data.
+template <typename I, typename D>
+class HipRowIter : public dmlc::RowBlockIter<I, D> {
+ public:
+  explicit HipRowIter(dmlc::Parser<I, D> *parser) {
+    std::unique_ptr<dmlc::Parser<I, D>> p(parser);
+    auto *hp = dynamic_cast<HipTextParser<I, D> *>(parser);
+    offset_.push_back(0);
+    while (p->Next()) {
+      const dmlc::RowBlock<I, D> &b = p->Value();
+      if (hp) Push(b, &hp->ValueCounts());
+      else Push(b, nullptr);
+      if (hp && hp->BlockStartsBatch()) {
+        max_index_ = std::max<uint64_t>(max_index_, hp->BatchMaxIndex());
+        max_field_ = std::max<uint64_t>(max_field_, hp->BatchMaxField());
+      }
+    }
+    row_.size = offset_.size() - 1;
+    row_.offset = offset_.data();
+    row_.label = dmlc::BeginPtr(label_);
+    row_.weight = dmlc::BeginPtr(weight_);
+    row_.qid = dmlc::BeginPtr(qid_);
+    row_.field = dmlc::BeginPtr(field_);
+    row_.index = dmlc::BeginPtr(index_);
+    row_.value = dmlc::BeginPtr(value_);
+  }
+  void BeforeFirst() override { at_head_ = true; }
+  bool Next() override {
+    if (!at_head_) return false;
+    at_head_ = false;
+    return true;
+  }
+  const dmlc::RowBlock<I, D> &Value() const override { return row_; }
+  size_t NumCol() const override { return static_cast<size_t>(static_cast<I>(max_index_)) + 1; }
+
+ private:
+  // RowBlockContainer::Push: labels (zeros for a block without them -- the
+  // reference copies from NULL there), weights / qids of the block's rows,
+  // entries with their maxima, offsets rebased.  With known counts only the
+  // block's own weights / qids are read (the reference reads `size` of them).
+  void Push(const dmlc::RowBlock<I, D> &b, const BlockCounts *k) {
+    const size_t ndata = b.offset[b.size] - b.offset[0];
+    const size_t nl = label_.size();
+    label_.resize(nl + b.size);
+    if (b.label) std::memcpy(label_.data() + nl, b.label, b.size * sizeof(D));
+    if (b.weight) weight_.insert(weight_.end(), b.weight, b.weight + (k ? k->weights : b.size));
+    if (b.qid) qid_.insert(qid_.end(), b.qid, b.qid + (k ? k->qids : b.size));
+    if (b.field) {
+      field_.insert(field_.end(), b.field, b.field + ndata);
+      if (!k)
+        for (size_t i = 0; i < ndata; ++i) max_field_ = std::max<uint64_t>(max_field_, b.field[i]);
+    }
+    index_.insert(index_.end(), b.index, b.index + ndata);
+    if (!k)
+      for (size_t i = 0; i < ndata; ++i) max_index_ = std::max<uint64_t>(max_index_, b.index[i]);
+    if (b.value) value_.insert(value_.end(), b.value, b.value + ndata);
+    const size_t shift = offset_.back();
+    for (size_t i = 0; i < b.size; ++i) offset_.push_back(shift + b.offset[i + 1] - b.offset[0]);
+  }
+
+  std::vector<size_t> offset_;
+  std::vector<D> label_, value_;
+  std::vector<float> weight_;
+  std::vector<uint64_t> qid_;
+  std::vector<I> index_, field_;
+  uint64_t max_index_ = 0, max_field_ = 0;
+  bool at_head_ = true;
+  dmlc::RowBlock<I, D> row_;
+};
+
+template <typename I, typename D>
+dmlc::RowBlockIter<I, D> *CreateIter_(const char *uri, unsigned part, unsigned nparts, const char *type) {
+  UriSpec spec(uri, part, nparts);
+  if (!spec.cache_file.empty())
+    LOG(WARNING) << "#" << spec.cache_file << ": the disk row cache is out of this build's scope; parsing in memory";
+  // as the reference (data.cc:88-105): the parser is created from spec.uri,
+  // i.e. WITHOUT the ?key=value arguments of the RowBlockIter uri
+  g_want_max_index = true;  // NumCol from the device maxima (this build's parsers)
+  dmlc::Parser<I, D> *parser;
+  try {
+    parser = CreateParser_<I, D>(spec.uri.c_str(), part, nparts, type);
+  } catch (...) {
+    g_want_max_index = false;
+    throw;
+  }
+  g_want_max_index = false;
+  return new HipRowIter<I, D>(parser);
+}
+
+}  // namespace
+}  // namespace dmlc_amd
+
+namespace dmlc {
+
+template <typename I, typename D>
+Parser<I, D> *Parser<I, D>::Create(const char *uri, unsigned part_index, unsigned num_parts, const char *type) {
+  return dmlc_amd::CreateParser_<I, D>(uri, part_index, num_parts, type);
+}
+template <typename I, typename D>
+RowBlockIter<I, D> *RowBlockIter<I, D>::Create(const char *uri, unsigned part_index, unsigned num_parts,
+                                               const char *type) {
+  return dmlc_amd::CreateIter_<I, D>(uri, part_index, num_parts, type);
+}
+
+template class Parser<uint32_t, real_t>;
+template class Parser<uint64_t, real_t>;
+template class Parser<uint32_t, int32_t>;
+template class Parser<uint64_t, int32_t>;
+template class Parser<uint32_t, int64_t>;
+template class Parser<uint64_t, int64_t>;
+template class RowBlockIter<uint32_t, real_t>;
+template class RowBlockIter<uint64_t, real_t>;
+template class RowBlockIter<uint32_t, int32_t>;
+template class RowBlockIter<uint64_t, int32_t>;
+template class RowBlockIter<uint32_t, int64_t>;
+template class RowBlockIter<uint64_t, int64_t>;
+
+// ---- registry (src/data.cc:189-227)
+typedef ParserFactoryReg<uint32_t, real_t> Reg32flt;
+typedef ParserFactoryReg<uint32_t, int32_t> Reg32int32;
+typedef ParserFactoryReg<uint32_t, int64_t> Reg32int64;
+typedef ParserFactoryReg<uint64_t, real_t> Reg64flt;
+typedef ParserFactoryReg<uint64_t, int32_t> Reg64int32;
+typedef ParserFactoryReg<uint64_t, int64_t> Reg64int64;
+DMLC_REGISTRY_ENABLE(Reg32flt);
+DMLC_REGISTRY_ENABLE(Reg32int32);
+DMLC_REGISTRY_ENABLE(Reg32int64);
+DMLC_REGISTRY_ENABLE(Reg64flt);
+DMLC_REGISTRY_ENABLE(Reg64int32);
+DMLC_REGISTRY_ENABLE(Reg64int64);
+
+DMLC_REGISTER_DATA_PARSER(uint32_t, real_t, libsvm, dmlc_amd::CreateLibSVMParser<uint32_t __DMLC_COMMA real_t>);
+DMLC_REGISTER_DATA_PARSER(uint64_t, real_t, libsvm, dmlc_amd::CreateLibSVMParser<uint64_t __DMLC_COMMA real_t>);
+DMLC_REGISTER_DATA_PARSER(uint32_t, real_t, libfm, dmlc_amd::CreateLibFMParser<uint32_t __DMLC_COMMA real_t>);
+DMLC_REGISTER_DATA_PARSER(uint64_t, real_t, libfm, dmlc_amd::CreateLibFMParser<uint64_t __DMLC_COMMA real_t>);
+DMLC_REGISTER_DATA_PARSER(uint32_t, real_t, csv, dmlc_amd::CreateCSVParser<uint32_t __DMLC_COMMA real_t>);
+DMLC_REGISTER_DATA_PARSER(uint64_t, real_t, csv, dmlc_amd::CreateCSVParser<uint64_t __DMLC_COMMA real_t>);
+DMLC_REGISTER_DATA_PARSER(uint32_t, int32_t, csv, dmlc_amd::CreateCSVParser<uint32_t __DMLC_COMMA int32_t>);
+DMLC_REGISTER_DATA_PARSER(uint64_t, int32_t, csv, dmlc_amd::CreateCSVParser<uint64_t __DMLC_COMMA int32_t>);
+DMLC_REGISTER_DATA_PARSER(uint32_t, int64_t, csv, dmlc_amd::CreateCSVParser<uint32_t __DMLC_COMMA int64_t>);
+DMLC_REGISTER_DATA_PARSER(uint64_t, int64_t, csv, dmlc_amd::CreateCSVParser<uint64_t __DMLC_COMMA int64_t>);
+
+}  // namespace dmlc

@@ -50,6 +50,8 @@ class TextSplit {
   void BeforeFirst();
   // Bytes of this part's byte range consumed so far.
   size_t BytesRead() const { return offset_curr_ - offset_begin_; }
+  // Bytes of the whole input (every part; InputSplit::GetTotalSize).
+  uint64_t TotalSize() const { return offset_.back(); }
 
  private:
   size_t Read(char *buf, size_t size);

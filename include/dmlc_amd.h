@@ -93,6 +93,10 @@ typedef struct dmlc_amd_params {
 /* Skip the single-pass uniform-grammar kernel and run the exact tile kernels
  * only (results are identical either way; this exists for testing/profiling). */
 #define DMLC_AMD_FLAG_EXACT 4u
+/* After the write pass, reduce the written index (and libfm field) arrays to
+ * their maxima in dmlc_amd_result.max_index / max_field (the NumCol of the
+ * reference's BasicRowIter, basic_row_iter.h:46-48). */
+#define DMLC_AMD_FLAG_MAX_INDEX 8u
 
 typedef struct dmlc_amd_csr {
   uint64_t *offset; /* rows + 1 (global, rebased across chunks) */
@@ -106,10 +110,14 @@ typedef struct dmlc_amd_csr {
 } dmlc_amd_csr;
 
 typedef struct dmlc_amd_result {
-  uint64_t count[8]; /* exact totals per slot, even when a capacity was exceeded */
-  uint64_t error;    /* 0, or (byte position << 16) | error code of the first error */
-  uint64_t path;     /* libsvm: 0 = single-pass uniform-grammar kernel, else exact tile kernels */
-  uint64_t reserved[6];
+  uint64_t count[8];  /* exact totals per slot, even when a capacity was exceeded */
+  uint64_t error;     /* 0, or (byte position << 16) | error code of the first error */
+  uint64_t path;      /* 0 = single-pass uniform-grammar kernel, else exact tile kernels
+                         (bit 1: the single-pass kernel handed over mid-launch) */
+  uint64_t max_index; /* with DMLC_AMD_FLAG_MAX_INDEX: largest index written (0 if none) --
+                         RowBlockContainer::max_index, row_block.h:126-168 */
+  uint64_t max_field; /* likewise for libfm field ids (max_field) */
+  uint64_t reserved[4];
 } dmlc_amd_result;
 
 /* Bytes of device workspace dmlc_amd_parse needs for this input. */

@@ -186,26 +186,42 @@ def _driver():
     return DRIVER
 
 
-def run_api(tmp_path, uri, part=0, nparts=1, fmt="libsvm", index_bits=32, dtype="f32", iter_=False):
+NTHREAD = 2  # the reference's factory thread count on a host with >= 12 processors (text_parser.h:32-35)
+
+
+def run_api(tmp_path, uri, part=0, nparts=1, fmt="libsvm", index_bits=32, dtype="f32", iter_=False,
+            nthread=NTHREAD, env=None):
     o = str(tmp_path / "out")
     args = [_driver(), uri, str(part), str(nparts), fmt, str(index_bits), dtype, o] + (["iter"] if iter_ else [])
-    r = subprocess.run(args, capture_output=True)
+    e = dict(os.environ, DMLC_AMD_NTHREAD=str(nthread), **(env or {}))
+    r = subprocess.run(args, capture_output=True, env=e)
     if r.returncode == 3:
         return {"error": open(o + ".error").read()}
+    assert r.returncode != 4, "a Parser block with offset[0] != 0"
     assert r.returncode == 0, r.stderr.decode()[-2000:]
     it = np.uint64 if index_bits == 64 else np.uint32
     vt = {"f32": np.float32, "i32": np.int32, "i64": np.int64}[dtype]
     h = {"offset": np.fromfile(o + ".offset", np.uint64), "label": np.fromfile(o + ".label", vt),
          "weight": np.fromfile(o + ".weight", np.float32), "qid": np.fromfile(o + ".qid", np.uint64),
          "index": np.fromfile(o + ".index", it), "value": np.fromfile(o + ".value", vt),
-         "field": np.fromfile(o + ".field", it), "meta": np.fromfile(o + ".meta", np.uint64)}
+         "field": np.fromfile(o + ".field", it), "meta": np.fromfile(o + ".meta", np.uint64),
+         "blocks": np.fromfile(o + ".blocks", np.uint64)}
     return h
 
 
-def oracle_files(contents, part=0, nparts=1, fmt=po.LIBSVM, **kw):
+def dir_order(d, contents):
+    """The files of directory d (written by _write from `contents`) in raw
+    readdir order, as the reference's InputSplit lists them (local_filesys.cc:98-122)."""
+    by_name = {"part-%02d.txt" % i: c for i, c in enumerate(contents)}
+    return [by_name[f] for f in os.listdir(d) if f in by_name]
+
+
+def oracle_files(contents, part=0, nparts=1, fmt=po.LIBSVM, nthread=NTHREAD, d=None, **kw):
+    if d is not None:
+        contents = dir_order(d, contents)
     chunks = po.split_text(contents, part, nparts)
     offs = np.cumsum([0] + [len(c) for c in chunks]).tolist()
-    return po.parse_chunks(b"".join(chunks), offs, fmt=fmt, **kw), len(chunks)
+    return po.parse_chunks(b"".join(chunks), offs, fmt=fmt, nthread=nthread, **kw), len(chunks)
 
 
 @pytest.mark.gpu
@@ -215,7 +231,7 @@ def test_api_unittest_inputsplit_scenarios(tmp_path):
     csv = [b"0,1,2,3\n4,5,6,7\n", b"8,9,10,11\n12,13,14,15", b"16,17,18,19\n"]
     d, _ = _write(tmp_path / "csv", csv)
     h = run_api(tmp_path, d, fmt="csv")
-    o, _ = oracle_files(csv, fmt=po.CSV)
+    o, _ = oracle_files(csv, fmt=po.CSV, d=d)
     assert "error" not in h and diff(h, o) == [] and len(h["offset"]) - 1 == 5
     # libsvm, no final newline (:70-92)
     svm = [b"1 1:1 2:2\n0 3:3\n1 4:4 5:5"]
@@ -232,7 +248,7 @@ def test_api_unittest_inputsplit_scenarios(tmp_path):
     rows = []
     for part in range(2):
         h = run_api(tmp_path, d, part, 2)
-        o, _ = oracle_files(five, part, 2)
+        o, _ = oracle_files(five, part, 2, d=d)
         assert diff(h, o) == []
         rows.append(len(h["offset"]) - 1)
     assert rows == [6, 4]
@@ -248,7 +264,7 @@ def test_api_synthetic_multifile_multipart(tmp_path, fmt):
     for nparts in (1, 3):
         for part in range(nparts):
             h = run_api(tmp_path, d, part, nparts, fmt)
-            o, nch = oracle_files(contents, part, nparts, fmt=po.LIBSVM if fmt == "libsvm" else po.CSV)
+            o, nch = oracle_files(contents, part, nparts, fmt=po.LIBSVM if fmt == "libsvm" else po.CSV, d=d)
             assert "error" not in h, (h, part, nparts, [len(c) for c in contents])
             assert diff(h, o) == [], (part, nparts)
 
@@ -266,11 +282,11 @@ def test_api_libfm_parser_and_rowiter(tmp_path):
     for bits in (32, 64):
         for uri, kw in ((d, {}), (d + "?indexing_mode=-1", {"indexing_mode": -1})):
             h = run_api(tmp_path, uri, fmt="libfm", index_bits=bits)
-            o, _ = oracle_files(contents, fmt=po.LIBFM, index_bits=bits, **kw)
+            o, _ = oracle_files(contents, fmt=po.LIBFM, index_bits=bits, d=d, **kw)
             assert "error" not in h, h
             assert len(h["field"]) == len(h["index"]) > 0 and diff(h, o) == [], (bits, uri)
     hi = run_api(tmp_path, d, fmt="libfm", iter_=True)
-    o, _ = oracle_files(contents, fmt=po.LIBFM)
+    o, _ = oracle_files(contents, fmt=po.LIBFM, d=d)
     assert diff(hi, o) == []
 
 
@@ -283,7 +299,9 @@ def test_api_large_multibatch_and_rowiter(tmp_path, monkeypatch):
     h = run_api(tmp_path, d)
     o, nch = oracle_files([text.tobytes()])
     assert diff(h, o) == []
-    assert int(h["meta"][0]) == nch and int(h["meta"][1]) == len(text)
+    # one block per non-empty FillData range, as ParserImpl::Next hands them out
+    assert h["blocks"].tolist() == o["blocks"]["rows"].tolist() and len(h["blocks"]) == 2 * nch
+    assert int(h["meta"][1]) == len(text)
     hi = run_api(tmp_path, d, iter_=True)
     assert diff(hi, o) == [] and int(hi["meta"][2]) == int(o["index"].max()) + 1
 
@@ -300,3 +318,52 @@ def test_api_errors_and_args(tmp_path):
     h = run_api(tmp_path, d3 + "?format=csv&label_column=0", fmt="auto")
     o, _ = oracle_files([b"1,2,3\n4,5,6\n"], fmt=po.CSV, label_column=0)
     assert diff(h, o) == []
+
+
+@pytest.mark.gpu
+def test_api_blocks_nthread_indexing_auto(tmp_path):
+    """FillData ranges through Parser::Create: nthread 1..3 (DMLC_AMD_NTHREAD),
+    indexing_mode=-1 decided per range, one block per non-empty range with
+    offset[0] == 0 -- equal to the oracle's blocks."""
+    lines = [b"1 0:1 2:3\n", b"0 5:1\n", b"1 1:2 7:1\n", b"0 3:4\n"] * 300
+    d, _ = _write(tmp_path / "idx", [b"".join(lines)])
+    for nt in (1, 2, 3):
+        for uri, kw in ((d, {}), (d + "?indexing_mode=-1", {"indexing_mode": -1})):
+            h = run_api(tmp_path, uri, nthread=nt)
+            o, _ = oracle_files([b"".join(lines)], nthread=nt, **kw)
+            assert "error" not in h and diff(h, o) == [], (nt, uri)
+            assert h["blocks"].tolist() == o["blocks"]["rows"].tolist(), (nt, uri)
+
+
+@pytest.mark.gpu
+def test_api_checks_registry_and_multi_worker(tmp_path):
+    """RowBlock / Row CHECKs and MemCostBytes with the reference's semantics,
+    a parser type registered by the calling program (DMLC_REGISTER_DATA_PARSER)
+    found by Parser::Create, and the pipeline with 1..4 workers per device
+    and small batches (parse-ahead, in-order delivery)."""
+    text, _ = synth.rows(synth.LIBSVM, 3000, 40, seed=6)
+    d, paths = _write(tmp_path / "api", [text.tobytes()])
+    r = subprocess.run([_driver(), "--api", paths[0]], capture_output=True)
+    assert r.returncode == 0, r.stderr.decode()[-2000:]
+    big, _ = synth.rows(synth.LIBSVM, 30000, 64, seed=8)
+    d2, _ = _write(tmp_path / "mw", [big.tobytes()])
+    o, _ = oracle_files([big.tobytes()])
+    for workers in ("1", "3"):
+        h = run_api(tmp_path, d2, env={"DMLC_AMD_WORKERS": workers, "DMLC_AMD_BATCH_BYTES": str(1 << 20)})
+        assert "error" not in h and diff(h, o) == [], workers
+        assert h["blocks"].tolist() == o["blocks"]["rows"].tolist()
+
+
+@pytest.mark.gpu
+def test_api_errors_raise_at_the_failing_block(tmp_path):
+    """A parse error in a later chunk surfaces after the blocks before it, as
+    the reference's ThreadedParser rethrows it at that chunk's Next()."""
+    good, _ = synth.rows(synth.LIBSVM, 20000, 32, seed=2)
+    d, _ = _write(tmp_path / "late", [good.tobytes() + b"1 -3:1\n"])
+    h = run_api(tmp_path, d, env={"DMLC_AMD_BATCH_BYTES": str(64 << 20)})
+    assert "sign == true" in h["error"]
+    # invalid batch-size settings fall back to the default instead of looping
+    d2, _ = _write(tmp_path / "ok2", [b"1 3:1\n"])
+    for bad in ("0", "abc"):
+        h = run_api(tmp_path, d2, env={"DMLC_AMD_BATCH_BYTES": bad})
+        assert h["index"].tolist() == [3], bad
