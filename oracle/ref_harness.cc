@@ -36,7 +36,8 @@ using dmlc::data::RowBlockContainer;
 // (text_parser.h:32-35): 1 in an 8-CPU build container, 2 on the 256-core GPU
 // host.  To run the genuine FillData range split with nthread > 1 here, this
 // test library answers omp_get_num_procs from DMLC_REF_NPROCS when that is set
-// (symbol interposition inside this .so), and forwards to libgomp otherwise.
+// (bound inside this .so by -Bsymbolic, oracle/Makefile, whatever OpenMP
+// runtime the process loaded first), and forwards to libgomp otherwise.
 extern "C" int omp_get_num_procs(void) {
   if (const char *e = std::getenv("DMLC_REF_NPROCS")) return std::atoi(e);
   using Fn = int (*)(void);
