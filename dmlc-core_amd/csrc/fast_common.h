@@ -652,14 +652,21 @@ DA_HDF void stage_commit(const uint8_t *text, uint64_t n, uint64_t tlo, const St
   }
 }
 
-// ---- decoupled look-back records: 8 words (one 64-byte line) per tile.
-// Word 0 = status (bits 62-63: 1 aggregate, 2 inclusive) | the tile's four
-// counts packed 15 bits each (a 16 KiB tile holds < 2^15 of anything);
-// words 1..4 = the inclusive prefix per counter, written and drained
-// (vmcnt(0)) before the status turns inclusive.  A reader polls ONE word per
-// predecessor and loads the inclusive words only from the one lane that
-// needs them -- polls are the bulk of this kernel's memory requests.
+// ---- decoupled look-back records.  Two arrays: st[ntiles], one 8-byte
+// status word per tile -- bits 62-63 state (1 aggregate, 2 inclusive) | the
+// tile's four counts packed 15 bits each (a 16 KiB tile holds < 2^15 of
+// anything) -- and incl[ntiles][4], the inclusive prefix per counter, written
+// and drained (vmcnt(0)) before the status turns inclusive.  The status words
+// of consecutive tiles share cache lines, so one look-back round polls 256
+// predecessors (4 polls per lane, 2 KiB, 32 lines) where a line per tile polled 64
+// (64 lines): the inclusive frontier the look-backs propagate advances up to
+// 256 tiles per round trip instead of 64 (the look-back was ~0.7 ms of the
+// 1M x 128 libsvm launch, measured by ablation).
 constexpr uint64_t kSAgg = 1ull << 62, kSIncl = 2ull << 62;
+#ifndef FSVM_LB_PER
+#define FSVM_LB_PER 1
+#endif
+constexpr int kLbPer = FSVM_LB_PER;  // predecessors polled per lane per round
 DA_HD uint64_t pack4(const uint32_t c[4]) {
   return (uint64_t)c[0] | ((uint64_t)c[1] << 15) | ((uint64_t)c[2] << 30) | ((uint64_t)c[3] << 45);
 }
@@ -670,59 +677,75 @@ DA_HD void drain_stores() {
 }
 
 // Lane 0: publish this tile's aggregate (tile 0 publishes its inclusive).
-DA_HD void publish_aggregate(uint64_t *lb, uint32_t k, const uint32_t cnt[4]) {
-  uint64_t *rec = lb + (uint64_t)k * 8;
+DA_HD void publish_aggregate(uint64_t *lb, uint32_t ntiles, uint32_t k, const uint32_t cnt[4]) {
+  uint64_t *st = lb, *incl = lb + ntiles;
   if (k == 0) {
-    for (int i = 0; i < 4; ++i) store_agent_u64(rec + 1 + i, cnt[i]);
+    for (int i = 0; i < 4; ++i) store_agent_u64(incl + i, cnt[i]);
     drain_stores();
-    store_agent_u64(rec, kSIncl | pack4(cnt));
+    store_agent_u64(st, kSIncl | pack4(cnt));
   } else {
-    store_agent_u64(rec, kSAgg | pack4(cnt));
+    store_agent_u64(st + k, kSAgg | pack4(cnt));
   }
 }
 
-// Wave 0: decoupled look-back.  Lane i polls predecessor j-1-i's status word;
-// a round consumes predecessors up to the first inclusive one and stops
-// before the first unpublished one.  cnt = this tile's counts (wave
+// Wave 0: decoupled look-back.  Poll i of lane l reads the status word of
+// predecessor j-1-(64 i + l) (each poll instruction reads 512 contiguous
+// bytes); a round consumes predecessors up to the first inclusive one and
+// stops before the first unpublished one.  cnt = this tile's counts (wave
 // uniform).  Ends with c.base[0..3] = exclusive prefixes, and publishes the
 // inclusive prefix.  Returns the number of rounds.  The caller synchronises.
 template <class BK>
-DA_HDF uint32_t look_back(uint64_t *lb, uint32_t k, const uint32_t cnt[4], uint32_t *gate, TileCommon &c,
-                          BK &bk) {
+DA_HDF uint32_t look_back(uint64_t *lb, uint32_t ntiles, uint32_t k, const uint32_t cnt[4], uint32_t *gate,
+                          TileCommon &c, BK &bk) {
   const uint32_t lane = bk.tid();
+  uint64_t *st = lb, *incl = lb + ntiles;
   uint64_t j = k;
   uint32_t spins = 0, rounds = 0;
   uint64_t acc[4] = {0, 0, 0, 0};
   bool done = k == 0;
   while (!done) {
     ++rounds;
-    uint64_t s = 0;
-    uint32_t st = 2;  // before tile 0: an inclusive 0
-    if (lane < j) {
-      s = load_agent_u64(lb + (j - 1 - lane) * 8);
-      st = (uint32_t)(s >> 62);
-    }
-    const uint64_t zero = bk.ballot(st == 0), incl = bk.ballot(st == 2);
-    const uint32_t fz = zero ? (uint32_t)ctz64(zero) : 64u, fi = incl ? (uint32_t)ctz64(incl) : 64u;
-    const uint32_t tagg = fi < fz ? fi : fz;  // lanes below contribute their aggregates
-    const uint64_t mine = lane < tagg ? s : 0ull;
+    uint64_t s[kLbPer];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) acc[i] += bk.wave_sum((uint32_t)((mine >> (15 * i)) & 0x7FFFu));
-    done = fi < fz;
-    if (done) {
-      if ((uint64_t)fi < j) {  // a real inclusive record (else: the start, 0)
-        if (lane == fi) {
-          const uint64_t *rec = lb + (j - 1 - fi) * 8;
-          for (int i = 0; i < 4; ++i) c.lbw[i] = load_agent_u64(const_cast<uint64_t *>(rec) + 1 + i);
-        }
+    for (int i = 0; i < kLbPer; ++i) {
+      const uint64_t d = (uint64_t)i * kWave + lane;  // predecessor j-1-d
+      s[i] = d < j ? load_agent_u64(st + (j - 1 - d)) : kSIncl;  // before tile 0: an inclusive 0
+    }
+    // the nearest stop: the smallest d whose word is unpublished or inclusive
+    uint64_t D = (uint64_t)kWave * kLbPer;  // predecessors that contribute their aggregates
+    bool stop_incl = false;
+#pragma unroll
+    for (int i = kLbPer - 1; i >= 0; --i) {
+      const uint32_t state = (uint32_t)(s[i] >> 62);
+      const uint64_t mz = bk.ballot(state == 0), mi = bk.ballot(state == 2);
+      if (mz | mi) {
+        const uint32_t f = (uint32_t)ctz64(mz | mi);
+        D = (uint64_t)i * kWave + f;
+        stop_incl = (mi >> f) & 1u;
+      }
+    }
+    uint32_t part[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < kLbPer; ++i) {
+      if ((uint64_t)i * kWave + lane < D) {
+#pragma unroll
+        for (int f = 0; f < 4; ++f) part[f] += (uint32_t)((s[i] >> (15 * f)) & 0x7FFFu);
+      }
+    }
+#pragma unroll
+    for (int f = 0; f < 4; ++f) acc[f] += bk.wave_sum(part[f]);
+    if (stop_incl) {
+      done = true;
+      if (D < j) {  // a real inclusive record (else: the start, 0)
+        if (lane < 4) c.lbw[lane] = load_agent_u64(incl + (j - 1 - D) * 4 + lane);
         bk.wave_sync();
 #pragma unroll
-        for (int i = 0; i < 4; ++i) acc[i] += c.lbw[i];
+        for (int f = 0; f < 4; ++f) acc[f] += c.lbw[f];
         bk.wave_sync();
       }
     } else {
-      j -= tagg;
-      if (tagg == 0) {
+      j -= D;
+      if (D == 0) {
         if (++spins > kSpinLimit) {  // never expected: hand the input to the exact path
           if (lane == 0) atomic_or_u32(gate, 2u);
           done = true;
@@ -733,15 +756,14 @@ DA_HDF uint32_t look_back(uint64_t *lb, uint32_t k, const uint32_t cnt[4], uint3
   }
   if (lane < 4) c.base[lane] = acc[lane == 0 ? 0 : lane == 1 ? 1 : lane == 2 ? 2 : 3];
   if (k > 0) {
-    uint64_t *rec = lb + (uint64_t)k * 8;
     if (lane < 4) {
       const uint64_t v = acc[lane == 0 ? 0 : lane == 1 ? 1 : lane == 2 ? 2 : 3];
       const uint32_t cv = cnt[lane == 0 ? 0 : lane == 1 ? 1 : lane == 2 ? 2 : 3];
-      store_agent_u64(rec + 1 + lane, v + cv);
+      store_agent_u64(incl + (uint64_t)k * 4 + lane, v + cv);
     }
     drain_stores();
     bk.wave_sync();
-    if (lane == 0) store_agent_u64(rec, kSIncl | pack4(cnt));
+    if (lane == 0) store_agent_u64(st + k, kSIncl | pack4(cnt));
   }
   return rounds;
 }

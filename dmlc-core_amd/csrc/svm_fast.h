@@ -463,7 +463,7 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
   // ---- publish this tile's aggregate
   const uint32_t cnt4[4] = {nL, nI, nV, nW};  // look-back slots Q_ROWS, Q_INDEX, Q_VALUE, Q_WEIGHT
   if (tid == 0) {
-    publish_aggregate(a.lb, k, cnt4);
+    publish_aggregate(a.lb, a.ntiles, k, cnt4);
     if (sh.c.bad) atomic_or_u32(a.gate, 1u);
   }
   // ---- first decode batch into registers (gives predecessors time to publish)
@@ -542,14 +542,18 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
     }
   }
   // ---- decoupled look-back by wave 0 (fast_common.h)
-#ifdef FSVM_ABL_NOLB  // timing ablation only: no look-back (wrong bases)
-  if (tid < 4) sh.c.base[tid] = 0;
-  if (false) {
+#ifdef FSVM_ABL_NOLB  // timing ablation only: write pass without look-back (bases k * counts, in bounds)
+  if (MODE == 2 && tid < 4) {
+    const int slot = tid == Q_ROWS ? C_ROWS : tid == Q_INDEX ? C_INDEX : tid == Q_VALUE ? C_VALUE : C_WEIGHT;
+    const uint64_t c = cnt4[tid], cap = a.cap[slot];
+    sh.c.base[tid] = cap > c + 64 ? mn<uint64_t>((uint64_t)k * c, cap - c - 64) : 0;
+  }
+  if (MODE != 2 && tid < kWave) {
 #else
   if (tid < kWave) {
 #endif
     const uint32_t rounds =
-        look_back(a.lb, k, cnt4, a.gate, sh.c, bk);
+        look_back(a.lb, a.ntiles, k, cnt4, a.gate, sh.c, bk);
 #if defined(DMLC_AMD_STAMPS) && defined(__HIP_DEVICE_COMPILE__)
     if (tid == 0 && k < kStampTiles) g_stamps[(uint64_t)k * 8 + 7] = rounds;
 #else
