@@ -497,6 +497,18 @@ DA_HD W16 win_at(const uint8_t *text, uint64_t tlo, uint64_t q) {
   return r;
 }
 
+// the same at tile offset o (position tlo + o)
+DA_HD W16 win_at_o(const uint8_t *text, uint32_t o) {
+  const uint32_t off = o + kPre;
+  const uint32_t *w = reinterpret_cast<const uint32_t *>(text + (off & ~3u));
+  const uint32_t sft = (off & 3u) * 8u;
+  const uint32_t x0 = w[0], x1 = w[1], x2 = w[2], x3 = w[3], x4 = w[4];
+  W16 r;
+  r.lo = funnel(x1, x0, sft) | ((uint64_t)funnel(x2, x1, sft) << 32);
+  r.hi = funnel(x3, x2, sft) | ((uint64_t)funnel(x4, x3, sft) << 32);
+  return r;
+}
+
 // ---- per-tile state every fast kernel keeps in LDS
 struct TileCommon {
   alignas(16) uint8_t text[kStage];  // position p <-> text[p - tlo + kPre]
@@ -657,11 +669,10 @@ DA_HDF void stage_commit(const uint8_t *text, uint64_t n, uint64_t tlo, const St
 // tile's four counts packed 15 bits each (a 16 KiB tile holds < 2^15 of
 // anything) -- and incl[ntiles][4], the inclusive prefix per counter, written
 // and drained (vmcnt(0)) before the status turns inclusive.  The status words
-// of consecutive tiles share cache lines, so one look-back round polls 256
-// predecessors (4 polls per lane, 2 KiB, 32 lines) where a line per tile polled 64
-// (64 lines): the inclusive frontier the look-backs propagate advances up to
-// 256 tiles per round trip instead of 64 (the look-back was ~0.7 ms of the
-// 1M x 128 libsvm launch, measured by ablation).
+// of consecutive tiles share cache lines: one poll instruction of a wave reads
+// 64 predecessors' words (512 contiguous bytes, 4 lines), where a record of a
+// line per tile cost a line per predecessor.  (kLbPer > 1 polls more
+// predecessors per round; measured slower at 4.)
 constexpr uint64_t kSAgg = 1ull << 62, kSIncl = 2ull << 62;
 #ifndef FSVM_LB_PER
 #define FSVM_LB_PER 1

@@ -34,14 +34,29 @@ enum : uint32_t { R_NONE = 0, R_L = 1, R_K = 2, R_I = 3 };
 // look-back counter slots (record words 0-3: aggregate, 4-7: inclusive prefix)
 enum { Q_ROWS = 0, Q_INDEX = 1, Q_VALUE = 2, Q_WEIGHT = 3 };
 
+struct Planes {  // slot 0: the segment before the tile; slot t+1: segment t
+  uint64_t d[kThreads + 1];  // digitchar
+  uint64_t n[kThreads + 1];  // newline
+  uint64_t c[kThreads + 1];  // ':'
+};
+// run list entries (tile offsets) that fit in the planes' space, which the
+// libsvm write pass no longer reads once the roles are known
+constexpr int kListCap = (int)(sizeof(Planes) / sizeof(uint16_t));
+// a pass of the run lists: the runs of consecutive segments, at most kPassRuns
+// before its last segment starts (a segment holds <= 64 run starts)
+constexpr uint32_t kPassRuns = (uint32_t)kListCap - kSegB;
+
 struct Shared {  // LDS of one workgroup
   TileCommon c;
   uint32_t cls[256];  // byte class table (fast_common.h class_of)
   DecTables dt;
-  uint64_t md[kThreads + 1];  // slot 0: the segment before the tile; slot t+1: segment t
-  uint64_t mn[kThreads + 1];
-  uint64_t mc[kThreads + 1];
-  uint16_t g16[kThreads + 1];  // digit plane, bytes 0-15 of segment t (t = kThreads: the post-halo)
+  union {
+    Planes m;
+    uint16_t lst[kListCap];
+  } u;
+  uint32_t gw[2 * kThreads + 2];  // digit plane as words: 2t, 2t+1 segment t; 2 kThreads: the post-halo
+  uint64_t pend[kTile / kPassRuns + 2];  // packed inclusive counts at the end of each pass
+  uint32_t npass;
 };
 
 struct Tile {
@@ -54,9 +69,9 @@ struct Tile {
     const uint64_t g0 = tlo >> 6;
     if (g < g0 + kThreads && (g >= g0 || (tlo > 0 && g + 1 == g0))) {
       const uint64_t s = g + 1 - g0;
-      *d = sh->md[s];
-      *n = sh->mn[s];
-      *c = sh->mc[s];
+      *d = sh->u.m.d[s];
+      *n = sh->u.m.n[s];
+      *c = sh->u.m.c[s];
       return;
     }
     // beyond the staged bytes (a gap or run longer than the pre-halo): a
@@ -168,7 +183,7 @@ DA_HD SegOut segment_roles(const Tile &t, int tid) {
   if (P >= a.n) return o;
   const int nv = (int)mn<uint64_t>(64, a.n - P);
   const uint64_t valid = nv == 64 ? ~0ull : ((1ull << nv) - 1);
-  const uint64_t D = t.sh->md[tid + 1], N = t.sh->mn[tid + 1], C = t.sh->mc[tid + 1];
+  const uint64_t D = t.sh->u.m.d[tid + 1], N = t.sh->u.m.n[tid + 1], C = t.sh->u.m.c[tid + 1];
   uint64_t S = 0;
   for (uint32_t i = 0; i < t.sh->c.ncs; ++i) {
     const uint64_t x = t.sh->c.csl[i];
@@ -178,7 +193,7 @@ DA_HD SegOut segment_roles(const Tile &t, int tid) {
   uint32_t dc = 0, ginl = 0, ginc = 0, prole = R_NONE;
   const uint64_t F = t.floor_of(P);
   if (P != F && !(F + 64 <= P &&
-                  carry_fast(t.sh->md[tid], t.sh->mn[tid], t.sh->mc[tid], &dc, &ginl, &ginc, &prole))) {
+                  carry_fast(t.sh->u.m.d[tid], t.sh->u.m.n[tid], t.sh->u.m.c[tid], &dc, &ginl, &ginc, &prole))) {
     dc = ginl = ginc = 0;
     prole = R_NONE;
     uint64_t d, n, c;
@@ -285,7 +300,7 @@ DA_HD SegOutFm segment_roles_fm(const Tile &t, int tid) {
   if (P >= a.n) return o;
   const int nv = (int)mn<uint64_t>(64, a.n - P);
   const uint64_t valid = nv == 64 ? ~0ull : ((1ull << nv) - 1);
-  const uint64_t D = t.sh->md[tid + 1], N = t.sh->mn[tid + 1], C = t.sh->mc[tid + 1];
+  const uint64_t D = t.sh->u.m.d[tid + 1], N = t.sh->u.m.n[tid + 1], C = t.sh->u.m.c[tid + 1];
   uint64_t S = 0;
   for (uint32_t i = 0; i < t.sh->c.ncs; ++i) {
     const uint64_t x = t.sh->c.csl[i];
@@ -384,7 +399,7 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
   stage_issue(a.text, a.n, t.tlo, sr, bk);  // text loads first: the chunk search overlaps them
   ChunkProbe cp;  // wave 0: the window load stays in flight through classification
   if (tid < kWave) cp = chunk_list_begin(a.cs, a.nchunk, t.tlo, bk);
-  if (tid == 0) sh.md[0] = sh.mn[0] = sh.mc[0] = 0;
+  if (tid == 0) sh.u.m.d[0] = sh.u.m.n[0] = sh.u.m.c[0] = 0;
   sh.cls[tid] = class_of((uint32_t)tid);
   init_dec_tables(sh.dt, bk);
   stage_commit(a.text, a.n, t.tlo, sr, sh.c, bk);
@@ -397,11 +412,10 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
   // ---- classify: segment tid -> slot tid+1; lanes 0..15 also one word each
   // of the 64 bytes before the tile -> slot 0
   uint32_t bad = 0;
-  uint64_t G;  // digit plane of my segment: the decoders' digit masks come from it
   {
     const Masks m = classify64_lut(sh.c.text + kPre + tid * kSegB, sh.cls);
-    G = m.g;
-    sh.g16[tid] = (uint16_t)m.g;
+    sh.gw[2 * tid] = (uint32_t)m.g;
+    sh.gw[2 * tid + 1] = (uint32_t)(m.g >> 32);
     if (tid == kWave) {  // digits of the 16 bytes after the tile (windows of my last runs)
       uint32_t g = 0;
 #pragma unroll
@@ -410,19 +424,19 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
         memcpy(&x, sh.c.text + kPre + kTile + 4 * i, 4);
         g |= classify_dword_lut(x, sh.cls).g << (4 * i);
       }
-      sh.g16[kThreads] = (uint16_t)g;
+      sh.gw[2 * kThreads] = g;
     }
-    sh.md[tid + 1] = m.d;
-    sh.mn[tid + 1] = m.n;
-    sh.mc[tid + 1] = m.c;
+    sh.u.m.d[tid + 1] = m.d;
+    sh.u.m.n[tid + 1] = m.n;
+    sh.u.m.c[tid + 1] = m.c;
     bad = m.bad;
     if (tid < 16 && t.tlo > 0) {
       uint32_t x;
       memcpy(&x, sh.c.text + 4 * tid, 4);
       const Nib b = classify_dword_lut(x, sh.cls);
-      atomic_or_u64(&sh.md[0], (uint64_t)b.d << (4 * tid));
-      atomic_or_u64(&sh.mn[0], (uint64_t)b.n << (4 * tid));
-      atomic_or_u64(&sh.mc[0], (uint64_t)b.c << (4 * tid));
+      atomic_or_u64(&sh.u.m.d[0], (uint64_t)b.d << (4 * tid));
+      atomic_or_u64(&sh.u.m.n[0], (uint64_t)b.n << (4 * tid));
+      atomic_or_u64(&sh.u.m.c[0], (uint64_t)b.c << (4 * tid));
     }
   }
   if (tid < kWave) chunk_list_end(a.cs, a.nchunk, t.tlo, t.thi, cp, sh.c, bk);
@@ -430,7 +444,7 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
   if (tid == 0) bad |= sh.c.toomany;
   FAST_STAMP(k, 3);
 #if defined(FSVM_ABL_STOP) && FSVM_ABL_STOP == 1  // timing ablation only: stage + classify
-  if (sh.md[tid + 1] == 0x123456789ull) a.res[15] = sh.mn[tid];
+  if (sh.u.m.d[tid + 1] == 0x123456789ull) a.res[15] = sh.u.m.n[tid];
   return;
 #endif
   // ---- roles, counts, eligibility
@@ -466,47 +480,49 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
     publish_aggregate(a.lb, a.ntiles, k, cnt4);
     if (sh.c.bad) atomic_or_u32(a.gate, 1u);
   }
-  // ---- first decode batch into registers (gives predecessors time to publish)
   const uint64_t P = t.tlo + (uint64_t)tid * kSegB;
   const bool one_chunk = sh.c.ncs == 0;  // no chunk boundary before cnext
-  // the window decoders are exact when its 16 bytes belong to the run's chunk
-  auto lim_of = [&](uint64_t q) { return one_chunk ? sh.c.cnext : t.next_cs(q); };
-  const uint64_t Gn = sh.g16[tid + 1];
-  // non-digit flags of the 16 window bytes at segment offset b (b < 64)
-  auto ndig16 = [&](uint32_t b) -> uint32_t {
-    const uint64_t x = (G >> b) | (b ? (Gn << (64u - b)) : 0ull);
-    return ~(uint32_t)x & 0xFFFFu;
+  // the window decoders are exact when their 16 bytes belong to the run's
+  // chunk: the chunk end after tile offset o, tile-relative (clamped)
+  const uint32_t lim1 = (uint32_t)mn<uint64_t>(sh.c.cnext - t.tlo, 0xFFFFFFFFull);
+  auto limr_of = [&](uint32_t o) -> uint32_t {
+    return one_chunk ? lim1 : (uint32_t)mn<uint64_t>(t.next_cs(t.tlo + o) - t.tlo, 0xFFFFFFFFull);
   };
-  auto dec_float = [&](uint64_t q) -> float {
+  auto lim_of = [&](uint64_t q) { return one_chunk ? sh.c.cnext : t.next_cs(q); };
+  // non-digit flags of the 16 window bytes at tile offset o (bits 16+ unused)
+  auto ndig_at = [&](uint32_t o) -> uint32_t {
+    const uint32_t i = o >> 5;
+    return ~funnel(sh.gw[i + 1], sh.gw[i], o & 31u);
+  };
+  // the decoders take the run's tile offset o (the run starts at tlo + o)
+  auto dec_float = [&](uint32_t o) -> float {
 #ifdef FSVM_ABL_NODEC  // timing ablation only (tools/build_variants.sh), never shipped
-    return (float)(uint32_t)q;
+    return (float)o;
 #endif
-    const uint64_t lim = lim_of(q);
     bool ok = false;
     float v = 0.f;
-    if (q + 16 <= lim) {
-      const W16 wq = win_at(sh.c.text, t.tlo, q);
+    if (o + 16u <= limr_of(o)) {
+      const W16 wq = win_at_o(sh.c.text, o);
       const uint32_t w4[4] = {(uint32_t)wq.lo, (uint32_t)(wq.lo >> 32), (uint32_t)wq.hi, (uint32_t)(wq.hi >> 32)};
-      v = wfloat32m(w4, ndig16((uint32_t)(q - P)), sh.dt, &ok);
+      v = wfloat32m(w4, ndig_at(o), sh.dt, &ok);
     }
-    if (!ok) v = slow_float(a.text, q, lim);
+    if (!ok) v = slow_float(a.text, t.tlo + o, lim_of(t.tlo + o));
     return v;
   };
-  auto dec_index = [&](uint64_t q) -> uint64_t {
+  auto dec_index = [&](uint32_t o) -> uint64_t {
 #ifdef FSVM_ABL_NODEC
-    return q;
+    return o;
 #endif
-    const uint64_t lim = lim_of(q);
     uint64_t v = 0;
     bool ok = false, pos = true;
-    if (q + 16 <= lim) {
-      const W16 wq = win_at(sh.c.text, t.tlo, q);
+    if (o + 16u <= limr_of(o)) {
+      const W16 wq = win_at_o(sh.c.text, o);
       const uint32_t w4[4] = {(uint32_t)wq.lo, (uint32_t)(wq.lo >> 32), (uint32_t)wq.hi, (uint32_t)(wq.hi >> 32)};
-      pos = wuint32m(w4, ndig16((uint32_t)(q - P)), sh.dt, &v, &ok);
+      pos = wuint32m(w4, ndig_at(o), sh.dt, &v, &ok);
     }
-    if (!ok) pos = slow_uint(a.text, q, lim, a.wide, &v);
+    if (!ok) pos = slow_uint(a.text, t.tlo + o, lim_of(t.tlo + o), a.wide, &v);
     if (!pos) {
-      raise_error(a.err, E_NEG_INDEX, q);
+      raise_error(a.err, E_NEG_INDEX, t.tlo + o);
       v = 0;
     }
     if (a.indexing_mode > 0) --v;
@@ -517,27 +533,79 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
 #endif
   constexpr int kB = FSVM_KB;  // runs per decoder decoded before the look-back
   static_assert(kB >= 1 && kB <= 5, "batch positions are packed 6 bits each");
-  // Values, labels and weights share the float decoder: one position-ordered
-  // stream of float runs per thread (a separate label pass cost every wave one
-  // more full float-decoder iteration for its ~2 labels).
   uint64_t ib[kB];
   float fb[kB];
-  uint32_t fpos = 0;  // bit positions of the batch's float runs, 6 bits each
+  // packed counts (fields as `mine`)
+  auto fL = [](uint64_t x) { return (uint32_t)(x & 0xFFFF); };
+  auto fW = [](uint64_t x) { return (uint32_t)((x >> 16) & 0xFFFF); };
+  auto fI = [](uint64_t x) { return (uint32_t)((x >> 32) & 0xFFFF); };
+  auto fV = [](uint64_t x) { return (uint32_t)(x >> 48); };
+
+  // ---- libsvm: run lists.  Every run's tile offset goes to an LDS list in
+  // output order -- indices, then values, labels, weights -- and the threads
+  // decode the lists round-robin: each wave decodes ceil(runs / 256) runs per
+  // list instead of its fullest lane's count, and the stores of consecutive
+  // lanes are consecutive.  The lists reuse the planes' LDS; a tile with more
+  // runs than fit is done in passes of consecutive segments.
+  uint32_t np = 1, mypass = 0;
+  uint64_t pe0 = totp;  // packed inclusive counts at the end of pass 0
+  auto build = [&](uint64_t s, uint64_t e) {  // my runs into the lists of the pass [s, e)
+    const uint64_t rel = ex - s, cn = e - s;
+    const uint32_t nIp = fI(cn), nVp = fV(cn), nLp = fL(cn);
+    const uint32_t o0 = (uint32_t)tid * kSegB;
+    uint32_t x = fI(rel);
+    for (uint64_t m = so.I; m; m &= m - 1) sh.u.lst[x++] = (uint16_t)(o0 + ctz64(m));
+    x = nIp + fV(rel);
+    for (uint64_t m = so.V; m; m &= m - 1) sh.u.lst[x++] = (uint16_t)(o0 + ctz64(m));
+    x = nIp + nVp + fL(rel);
+    for (uint64_t m = so.L; m; m &= m - 1) sh.u.lst[x++] = (uint16_t)(o0 + ctz64(m));
+    x = nIp + nVp + nLp + fW(rel);
+    for (uint64_t m = so.W; m; m &= m - 1) sh.u.lst[x++] = (uint16_t)(o0 + ctz64(m));
+  };
+  uint32_t fpos = 0;  // libfm: bit positions of the batch's float runs, 6 bits each
   uint64_t mI = so.I, mF = so.V | so.L | so.W;
   if (MODE == 2) {
-#pragma unroll
-    for (int u = 0; u < kB; ++u) {
-      ib[u] = 0;
-      fb[u] = 0.f;
-      if (mI) {
-        ib[u] = dec_index(P + ctz64(mI));
-        mI &= mI - 1;
+    if constexpr (!FM) {
+      // (the block scan's barriers ordered every plane read before these writes)
+      if (nL + nW + nI + nV > kPassRuns) {  // block-uniform: several passes
+        const uint32_t own = fL(mine) + fW(mine) + fI(mine) + fV(mine);
+        const uint32_t tex = fL(ex) + fW(ex) + fI(ex) + fV(ex);
+        mypass = tex / kPassRuns;
+        if (tid == kThreads - 1 || (tex + own) / kPassRuns != mypass) sh.pend[mypass] = ex + mine;
+        if (tid == kThreads - 1) sh.npass = mypass + 1;
+        bk.sync();
+        np = sh.npass;
+        pe0 = sh.pend[0];
       }
-      if (mF) {
-        const uint32_t bpos = (uint32_t)ctz64(mF);
-        fb[u] = dec_float(P + bpos);
-        fpos |= bpos << (6 * u);
-        mF &= mF - 1;
+      if (mypass == 0) build(0, pe0);
+      bk.sync();
+      // ---- first decode batch into registers (gives predecessors time to publish)
+      const uint32_t nI0 = fI(pe0), nF0 = fV(pe0) + fL(pe0) + fW(pe0);
+#pragma unroll
+      for (int u = 0; u < kB; ++u) {
+        const uint32_t j = (uint32_t)tid + (uint32_t)u * kThreads;
+        ib[u] = 0;
+        fb[u] = 0.f;
+        if (j < nI0) ib[u] = dec_index(sh.u.lst[j]);
+        if (j < nF0) fb[u] = dec_float(sh.u.lst[nI0 + j]);
+      }
+    } else {
+      // libfm: each thread decodes its own segment's runs (values, labels and
+      // weights in one position-ordered float stream)
+#pragma unroll
+      for (int u = 0; u < kB; ++u) {
+        ib[u] = 0;
+        fb[u] = 0.f;
+        if (mI) {
+          ib[u] = dec_index((uint32_t)(P - t.tlo) + ctz64(mI));
+          mI &= mI - 1;
+        }
+        if (mF) {
+          const uint32_t bpos = (uint32_t)ctz64(mF);
+          fb[u] = dec_float((uint32_t)(P - t.tlo) + bpos);
+          fpos |= bpos << (6 * u);
+          mF &= mF - 1;
+        }
       }
     }
   }
@@ -585,10 +653,8 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
   }
   if (MODE != 2) return;
 
-  // ---- stores: the register batch, then the rest of this segment's runs,
-  // one role at a time (no divergence between the index and value decoders)
-  const uint64_t eL = bRows + (ex & 0xFFFF), eW = bW + ((ex >> 16) & 0xFFFF),
-                 eI = bIdx + ((ex >> 32) & 0xFFFF), eV = bVal + (ex >> 48);
+  // ---- stores
+  const uint64_t eL = bRows + fL(ex), eW = bW + fW(ex), eI = bIdx + fI(ex), eV = bVal + fV(ex);
   auto put_index = [&](uint64_t r, uint64_t v, uint64_t q) {
 #ifdef FSVM_ABL_NOSTORE  // timing ablation only
     if (v == 0x123456789ull) a.res[15] = r;
@@ -609,7 +675,60 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
     if (r < a.cap[C_VALUE]) a.value[r] = v;
     else raise_error(a.err, E_CAPACITY, q);
   };
-  {
+  auto put_label = [&](uint64_t r, float v, uint64_t q) {
+    if (r < a.cap[C_ROWS]) a.label[r] = v;
+    else raise_error(a.err, E_CAPACITY, q);
+  };
+  auto put_weight = [&](uint64_t r, float v, uint64_t q) {
+    if (r < a.cap[C_WEIGHT]) a.weight[r] = v;
+    else raise_error(a.err, E_CAPACITY, q);
+  };
+  if constexpr (!FM) {
+    // entry j of the float list of the pass starting at packed counts s
+    auto put_float = [&](uint32_t j, float v, uint32_t o, uint64_t s, uint32_t nVp, uint32_t nLp) {
+      const uint64_t q = t.tlo + o;
+      if (j < nVp) put_value(bVal + fV(s) + j, v, q);
+      else if (j < nVp + nLp) put_label(bRows + fL(s) + (j - nVp), v, q);
+      else put_weight(bW + fW(s) + (j - nVp - nLp), v, q);
+    };
+    {  // the register batch (pass 0)
+      const uint32_t nI0 = fI(pe0), nV0 = fV(pe0), nL0 = fL(pe0), nF0 = nV0 + nL0 + fW(pe0);
+#pragma unroll
+      for (int u = 0; u < kB; ++u) {
+        const uint32_t j = (uint32_t)tid + (uint32_t)u * kThreads;
+        if (j < nI0) put_index(bIdx + j, ib[u], t.tlo + sh.u.lst[j]);
+        if (j < nF0) put_float(j, fb[u], sh.u.lst[nI0 + j], 0, nV0, nL0);
+      }
+    }
+    for (uint32_t p = 0; p < np; ++p) {
+      const uint64_t s = p ? sh.pend[p - 1] : 0, e = p ? sh.pend[p] : pe0;
+      if (p) {  // block-uniform
+        bk.sync();
+        if (mypass == p) build(s, e);
+        bk.sync();
+      }
+      const uint64_t cn = e - s;
+      const uint32_t nIp = fI(cn), nVp = fV(cn), nLp = fL(cn), nFp = nVp + nLp + fW(cn);
+      const uint32_t j0 = (uint32_t)tid + (p ? 0u : (uint32_t)kB * kThreads);
+      for (uint32_t j = j0; j < nIp; j += kThreads) {
+        const uint32_t o = sh.u.lst[j];
+        put_index(bIdx + fI(s) + j, dec_index(o), t.tlo + o);
+      }
+      for (uint32_t j = j0; j < nFp; j += kThreads) {
+        const uint32_t o = sh.u.lst[nIp + j];
+        put_float(j, dec_float(o), o, s, nVp, nLp);
+      }
+    }
+    // each row's offset: the indices before its label
+    uint64_t rl = eL;
+    for (uint64_t m = so.L; m; m &= m - 1, ++rl) {
+      const uint64_t below = (m & (0 - m)) - 1;
+      if (rl < a.cap[C_ROWS]) a.offset[rl] = eI + popc64(so.I & below);
+      else raise_error(a.err, E_CAPACITY, P + ctz64(m));
+    }
+  } else {
+    // libfm: the register batch, then the rest of this segment's runs, one
+    // role at a time (no divergence between the index and value decoders)
     const uint32_t nIm = (uint32_t)popc64(so.I), nFm = (uint32_t)popc64(so.V | so.L | so.W);
     uint64_t rv = eV, rl = eL, rw = eW;  // this thread's running output ranks
     auto put_float = [&](uint32_t bpos, float v) {
@@ -625,9 +744,7 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
         }
         ++rl;
       } else {
-        if (rw < a.cap[C_WEIGHT]) a.weight[rw] = v;
-        else raise_error(a.err, E_CAPACITY, q);
-        ++rw;
+        put_weight(rw++, v, q);
       }
     };
 #pragma unroll
@@ -636,15 +753,13 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
       if ((uint32_t)u < nFm) put_float((fpos >> (6 * u)) & 63u, fb[u]);
     }
     for (uint64_t r = eI + kB; mI; mI &= mI - 1, ++r) {
-      const uint64_t q = P + ctz64(mI);
-      put_index(r, dec_index(q), q);
+      const uint32_t o = (uint32_t)(P - t.tlo) + ctz64(mI);
+      put_index(r, dec_index(o), t.tlo + o);
     }
     for (; mF; mF &= mF - 1) {
       const uint32_t bpos = (uint32_t)ctz64(mF);
-      put_float(bpos, dec_float(P + bpos));
+      put_float(bpos, dec_float((uint32_t)(P - t.tlo) + bpos));
     }
-  }
-  if constexpr (FM) {
     // every v1 is decoded by the reference: a '-' field is the sign error
     // even when its triple is dropped (strtonum.h:416, libfm_parser.h:104)
     for (uint64_t m = soF; m; m &= m - 1) {

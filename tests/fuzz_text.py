@@ -73,6 +73,26 @@ def uniform_libsvm(rng, nlines, maxfeat=40, violate=False):
     return text.encode("latin-1")
 
 
+def dense_libsvm(rng, nbytes, style):
+    """libsvm text with the shortest runs the grammar allows, so a 16 KiB tile
+    holds several thousand runs (the fast kernel's run lists then take
+    several passes): 'pairs' "1:2 3:4 ...", 'weights' "l:w i:v ...",
+    'labels' one-digit label-only lines, 'mixed' all of them."""
+    out, n = [], 0
+    while n < nbytes:
+        st = style if style != "mixed" else ("pairs", "weights", "labels")[int(rng.integers(0, 3))]
+        d = lambda: str(int(rng.integers(0, 10)))
+        if st == "labels":
+            line = d()
+        elif st == "weights":
+            line = d() + ":" + d() + "".join(" %s:%s" % (d(), d()) for _ in range(int(rng.integers(1, 40))))
+        else:
+            line = d() + "".join(" %s:%s" % (d(), d()) for _ in range(int(rng.integers(1, 60))))
+        out.append(line)
+        n += len(line) + 1
+    return ("\n".join(out) + "\n").encode("latin-1")
+
+
 def _csv_field(rng):
     r = rng.random()
     if r < 0.08:

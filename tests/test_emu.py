@@ -142,6 +142,18 @@ def test_emu_fast_multi_tile():
             assert h["path"] == "fast"
 
 
+def test_emu_fast_dense_runs():
+    """Tiles with thousands of one-byte runs: the run lists of the libsvm
+    write pass overflow the planes' LDS and are decoded in passes
+    (svm_fast.h kPassRuns); labels, weights and values across the pass seams."""
+    rng = np.random.default_rng(91)
+    for it, style in enumerate(("pairs", "weights", "labels", "mixed")):
+        data = fuzz_text.dense_libsvm(rng, 3 * 16384 + 777, style)
+        offs = fuzz_text.random_cuts(rng, data, 4, anywhere=False)
+        h = _emu_vs_oracle(data, offs, **({"index_bits": 64} if it == 1 else {}))
+        assert h["path"] == "fast", style
+
+
 def test_emu_fast_equals_exact_synthetic():
     text, _ = synth.rows(synth.LIBSVM, 800, 40, seed=5)
     data = text.tobytes()

@@ -250,6 +250,18 @@ def test_gpu_fast_multi_tile_vs_oracle(dm):
             assert h["path"] == "fast", it
 
 
+def test_gpu_fast_dense_runs_vs_oracle(dm):
+    """Thousands of one-byte runs per 16 KiB tile: the libsvm write pass
+    decodes its run lists in several passes (svm_fast.h kPassRuns)."""
+    rng = np.random.default_rng(1212)
+    for it, style in enumerate(("pairs", "weights", "labels", "mixed", "pairs", "mixed")):
+        data = fuzz_text.dense_libsvm(rng, int(rng.integers(3, 40)) * 16384 + int(rng.integers(0, 999)), style)
+        offs = fuzz_text.random_cuts(rng, data, int(rng.integers(0, 12)), anywhere=False)
+        kw = {"index_bits": 64} if it % 2 else {}
+        h = _gpu_vs_oracle_paths(dm, data, offs, **kw)
+        assert h["path"] == "fast", (it, style)
+
+
 def test_gpu_fast_synthetic_vs_oracle(dm):
     """~100 MB of canonical synthetic text (many tiles, 8 MiB InputSplit chunks)."""
     text, _ = synth.rows(synth.LIBSVM, 50000, 128, seed=21)

@@ -6,8 +6,8 @@ O=$R/gpurun_out/abpmc
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
 for v in ${VARIANTS}; do
-  DMLC_AMD_LIB=$R/dmlc-core_amd/lib/variants/$v.so timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_WAVE_CYCLES --kernel-trace --output-format csv -d $O/$v -o run -- python3 $R/tools/time_variant.py ${FMT:-libsvm} > $O/$v.log 2>&1 || { tail -5 $O/$v.log; exit 1; }
-  python3 - "$O/$v" "$v" <<'PY'
+  DMLC_AMD_LIB=$R/dmlc-core_amd/lib/variants/$v.so timeout -s KILL 120 rocprofv3 --pmc ${COUNTERS:-SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_WAVE_CYCLES} --kernel-trace --output-format csv -d $O/$v${SFX} -o run -- python3 $R/tools/time_variant.py ${FMT:-libsvm} > $O/$v${SFX}.log 2>&1 || { tail -5 $O/$v.log; exit 1; }
+  python3 - "$O/$v${SFX}" "$v${SFX}" <<'PY'
 import csv, glob, sys, collections
 f = glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive=True)
 acc = collections.defaultdict(list)
