@@ -26,15 +26,16 @@ constexpr uint32_t kSpinLimit = 1u << 22;
 // of each tile records s_memtime at phase boundaries into g_stamps; the
 // product build executes no stamp.
 constexpr uint32_t kStampTiles = 1u << 17;
+constexpr uint32_t kStampSlots = 16;  // per tile: 0 realtime start, 1.. phase ends, 15 look-back rounds
 #if defined(DMLC_AMD_STAMPS) && defined(__HIPCC__)
-__device__ uint64_t g_stamps[kStampTiles * 8];
+__device__ uint64_t g_stamps[kStampTiles * kStampSlots];
 #endif
 #if defined(DMLC_AMD_STAMPS) && defined(__HIP_DEVICE_COMPILE__)
 #define FAST_STAMP(k, i)                                                         \
   do {                                                                           \
     if (tid == 0 && (k) < kStampTiles) {                                         \
       __builtin_amdgcn_sched_barrier(0);                                         \
-      g_stamps[(uint64_t)(k) * 8 + (i)] =                                        \
+      g_stamps[(uint64_t)(k) * kStampSlots + (i)] =                                        \
           (i) == 0 ? __builtin_amdgcn_s_memrealtime() : __builtin_amdgcn_s_memtime(); \
       __builtin_amdgcn_sched_barrier(0);                                         \
     }                                                                            \
@@ -394,10 +395,9 @@ DA_HD uint32_t dig4(uint32_t d, uint32_t acc) {
 DA_HD uint32_t nd4(uint32_t x) {  // 4 bits: byte i is not '0'..'9' (bytes < 0x80)
   return udot4((((x ^ 0x30303030u) + 0x76767676u) >> 7) & 0x01010101u, 0x08040201u, 0u);
 }
-DA_HD uint32_t byte_of(const uint32_t w[4], uint32_t p) {  // window byte p < 16
-  const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3];
-  const uint32_t a = (p & 4u) ? w1 : w0, b = (p & 4u) ? w3 : w2;
-  return ((p & 8u ? b : a) >> (8u * (p & 3u))) & 0xFFu;
+DA_HD uint32_t byte_of(const uint32_t w[4], uint32_t p) {  // window byte p < 16 (one v_perm)
+  const uint32_t hi = (p & 8u) ? w[3] : w[1], lo = (p & 8u) ? w[2] : w[0];
+  return perm_b32(hi, lo, (p & 7u) | 0x0C0C0C00u);
 }
 DA_HD uint64_t low_bytes(uint32_t k) {  // mask of the low k bytes, k <= 8
   return k >= 8 ? ~0ull : ((1ull << (8u * k)) - 1ull);

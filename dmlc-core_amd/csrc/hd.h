@@ -106,10 +106,26 @@ DA_HD uint32_t perm_b32(uint32_t s0, uint32_t s1, uint32_t sel) {
 #if defined(__HIP_DEVICE_COMPILE__)
   return __builtin_amdgcn_perm(s0, s1, sel);
 #else
+  // V_PERM_B32: selector byte 0-7 picks a byte of {s0:s1}; 8-11 replicate
+  // the sign bit of bytes 1, 3 of s1 and 1, 3 of s0; 12 gives 0x00, 13+ 0xFF
   const uint64_t src = ((uint64_t)s0 << 32) | s1;
   uint32_t r = 0;
-  for (int i = 0; i < 4; ++i) r |= (uint32_t)((src >> (8 * ((sel >> (8 * i)) & 7))) & 0xFF) << (8 * i);
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t k = (sel >> (8 * i)) & 0xFFu;
+    uint32_t b;
+    if (k < 8) b = (uint32_t)(src >> (8 * k)) & 0xFFu;
+    else if (k < 12) b = ((src >> (16 * (k - 8) + 15)) & 1u) ? 0xFFu : 0u;
+    else b = k == 12 ? 0u : 0xFFu;
+    r |= b << (8 * i);
+  }
   return r;
+#endif
+}
+
+// compiler scheduling barrier (device): no instruction moves across it
+DA_HD void sched_fence() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_sched_barrier(0);
 #endif
 }
 

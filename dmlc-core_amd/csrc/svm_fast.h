@@ -494,39 +494,52 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
     const uint32_t i = o >> 5;
     return ~funnel(sh.gw[i + 1], sh.gw[i], o & 31u);
   };
-  // the decoders take the run's tile offset o (the run starts at tlo + o)
-  auto dec_float = [&](uint32_t o) -> float {
+  // The decoders take the run's tile offset o (the run starts at tlo + o).
+  // win_*: the branch-free window form; *ok = false sends the run to the
+  // byte decoders (slow_*), which also raise the sign error.
+  auto win_float = [&](uint32_t o, bool *ok) -> float {
 #ifdef FSVM_ABL_NODEC  // timing ablation only (tools/build_variants.sh), never shipped
+    *ok = true;
     return (float)o;
 #endif
-    bool ok = false;
-    float v = 0.f;
-    if (o + 16u <= limr_of(o)) {
-      const W16 wq = win_at_o(sh.c.text, o);
-      const uint32_t w4[4] = {(uint32_t)wq.lo, (uint32_t)(wq.lo >> 32), (uint32_t)wq.hi, (uint32_t)(wq.hi >> 32)};
-      v = wfloat32m(w4, ndig_at(o), sh.dt, &ok);
-    }
-    if (!ok) v = slow_float(a.text, t.tlo + o, lim_of(t.tlo + o));
+    const W16 wq = win_at_o(sh.c.text, o);
+    const uint32_t w4[4] = {(uint32_t)wq.lo, (uint32_t)(wq.lo >> 32), (uint32_t)wq.hi, (uint32_t)(wq.hi >> 32)};
+    bool k1;
+    const float v = wfloat32m(w4, ndig_at(o), sh.dt, &k1);
+    *ok = k1 && o + 16u <= limr_of(o);
     return v;
   };
-  auto dec_index = [&](uint32_t o) -> uint64_t {
+  auto win_index = [&](uint32_t o, bool *ok) -> uint64_t {
 #ifdef FSVM_ABL_NODEC
+    *ok = true;
     return o;
 #endif
+    const W16 wq = win_at_o(sh.c.text, o);
+    const uint32_t w4[4] = {(uint32_t)wq.lo, (uint32_t)(wq.lo >> 32), (uint32_t)wq.hi, (uint32_t)(wq.hi >> 32)};
+    uint64_t v;
+    bool k1;
+    const bool pos = wuint32m(w4, ndig_at(o), sh.dt, &v, &k1);
+    *ok = k1 && pos && o + 16u <= limr_of(o);
+    return a.indexing_mode > 0 ? v - 1 : v;
+  };
+  auto slow_flt = [&](uint32_t o) -> float { return slow_float(a.text, t.tlo + o, lim_of(t.tlo + o)); };
+  auto slow_idx = [&](uint32_t o) -> uint64_t {
     uint64_t v = 0;
-    bool ok = false, pos = true;
-    if (o + 16u <= limr_of(o)) {
-      const W16 wq = win_at_o(sh.c.text, o);
-      const uint32_t w4[4] = {(uint32_t)wq.lo, (uint32_t)(wq.lo >> 32), (uint32_t)wq.hi, (uint32_t)(wq.hi >> 32)};
-      pos = wuint32m(w4, ndig_at(o), sh.dt, &v, &ok);
-    }
-    if (!ok) pos = slow_uint(a.text, t.tlo + o, lim_of(t.tlo + o), a.wide, &v);
-    if (!pos) {
+    if (!slow_uint(a.text, t.tlo + o, lim_of(t.tlo + o), a.wide, &v)) {
       raise_error(a.err, E_NEG_INDEX, t.tlo + o);
       v = 0;
     }
-    if (a.indexing_mode > 0) --v;
-    return v;
+    return a.indexing_mode > 0 ? v - 1 : v;
+  };
+  auto dec_float = [&](uint32_t o) -> float {
+    bool ok;
+    const float v = win_float(o, &ok);
+    return ok ? v : slow_flt(o);
+  };
+  auto dec_index = [&](uint32_t o) -> uint64_t {
+    bool ok;
+    const uint64_t v = win_index(o, &ok);
+    return ok ? v : slow_idx(o);
   };
 #ifndef FSVM_KB
 #define FSVM_KB 4
@@ -579,6 +592,7 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
       }
       if (mypass == 0) build(0, pe0);
       bk.sync();
+      FAST_STAMP(k, 5);
       // ---- first decode batch into registers (gives predecessors time to publish)
       const uint32_t nI0 = fI(pe0), nF0 = fV(pe0) + fL(pe0) + fW(pe0);
 #pragma unroll
@@ -589,6 +603,7 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
         if (j < nI0) ib[u] = dec_index(sh.u.lst[j]);
         if (j < nF0) fb[u] = dec_float(sh.u.lst[nI0 + j]);
       }
+      FAST_STAMP(k, 6);
     } else {
       // libfm: each thread decodes its own segment's runs (values, labels and
       // weights in one position-ordered float stream)
@@ -623,7 +638,7 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
     const uint32_t rounds =
         look_back(a.lb, a.ntiles, k, cnt4, a.gate, sh.c, bk);
 #if defined(DMLC_AMD_STAMPS) && defined(__HIP_DEVICE_COMPILE__)
-    if (tid == 0 && k < kStampTiles) g_stamps[(uint64_t)k * 8 + 7] = rounds;
+    if (tid == 0 && k < kStampTiles) g_stamps[(uint64_t)k * kStampSlots + 15] = rounds;
 #else
     (void)rounds;
 #endif
@@ -632,7 +647,7 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
 #endif
   }
   bk.sync();
-  FAST_STAMP(k, 5);
+  FAST_STAMP(k, 7);
 #if defined(FSVM_ABL_STOP) && FSVM_ABL_STOP == 3  // + first decode batch + look-back
   if (sh.c.base[0] == 0x123456789ull) a.res[15] = (uint64_t)ib[0] + (uint64_t)fb[0];
   return;
@@ -793,7 +808,7 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
       }
     }
   }
-  FAST_STAMP(k, 6);
+  FAST_STAMP(k, 8);
   // ---- per-chunk exclusive counts at each chunk start in my segment
   if (a.chunk_tab) {
     for (uint32_t i = 0; i < sh.c.ncs; ++i) {

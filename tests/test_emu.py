@@ -142,6 +142,21 @@ def test_emu_fast_multi_tile():
             assert h["path"] == "fast"
 
 
+def test_window_decoders_vs_byte_decoders():
+    """The 16-byte window decoders (fast_common.h wfloat32m / wuint32m, the
+    fast kernels' number conversion) against the exact byte decoders on 2M
+    generated number strings: every string the window form accepts decodes
+    bit-identically (tests/emu/dec_check.cpp)."""
+    import os
+    import subprocess
+    pyemu.build()
+    exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "emu", "_build", "dec_check")
+    r = subprocess.run([exe, "2000000", "7"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:]
+    fast_f = int(r.stdout.split("float fast ")[1].split(",")[0])
+    assert fast_f > 1000000, r.stdout
+
+
 def test_emu_fast_dense_runs():
     """Tiles with thousands of one-byte runs: the run lists of the libsvm
     write pass overflow the planes' LDS and are decoded in passes

@@ -3,7 +3,7 @@
 Loads dmlc-core_amd/lib/libdmlc_amd_stamps.so (make -C dmlc-core_amd stamps),
 parses a synthetic shard, and prints the mean shader cycles each tile spends
 per phase: 1->2 staging, 2->3 classify, 3->4 roles + block scan,
-4->5 look-back, 5->6 decode + stores.  Stamp values never feed an output.
+4->5 run lists, 5->6 first decode batch, 6->7 look-back, 7->8 stores.  Stamp values never feed an output.
 """
 import ctypes
 import os
@@ -17,7 +17,8 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "dmlc-core_amd", "python")]
 import dmlc_amd  # noqa: E402
 from tools import synth  # noqa: E402
 
-PHASES = ["stage", "classify", "roles+scan", "look-back", "decode+store"]
+PHASES = ["stage", "classify", "roles+scan", "lists", "batch decode", "look-back", "stores"]
+SLOTS = 16
 
 
 def main():
@@ -45,10 +46,10 @@ def main():
             else:
                 p.parse_into(d_text, d_cs, out, res)
         torch.cuda.synchronize()
-        st = np.zeros(n * 8, dtype=np.uint64)
+        st = np.zeros(n * SLOTS, dtype=np.uint64)
         assert L.dmlc_amd_debug_stamps(st.ctypes.data, st.nbytes) == 0
-        st = st.reshape(n, 8).astype(np.int64)
-        last = 6 if mode == "full" else 5
+        st = st.reshape(n, SLOTS).astype(np.int64)
+        last = 8 if mode == "full" else 4
         d = np.diff(st[:, 1:last + 1], axis=1)
         rt = st[:, 0]
         print("%s: %d tiles, wall span of tile starts %.3f ms (100 MHz clock)"
@@ -58,7 +59,7 @@ def main():
             print("  %-14s mean %8.0f cyc  p50 %8.0f  p99 %8.0f" % (PHASES[i], col.mean(), np.median(col),
                                                                    np.percentile(col, 99)))
         print("  total          mean %8.0f cyc" % d.sum(axis=1).mean())
-        rounds = st[:, 7]
+        rounds = st[:, 15]
         print("  look-back rounds: mean %.2f p50 %.0f p99 %.0f max %d"
               % (rounds.mean(), np.median(rounds), np.percentile(rounds, 99), rounds.max()))
 
