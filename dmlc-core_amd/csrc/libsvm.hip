@@ -29,6 +29,10 @@ template <int MODE>
 __global__ void __launch_bounds__(kThreads, FSVM_MINW) svm_fast_tile(FastSvmArgs a) {
   __shared__ __attribute__((aligned(16))) fsvm::Shared sh;
   __shared__ uint64_t scratch[kBlockScratchU64];
+#ifdef FSVM_ABL_PAD_LDS  // occupancy experiment only: pad the workgroup's LDS
+  __shared__ uint32_t pad[FSVM_ABL_PAD_LDS / 4];
+  if (a.n == 1) pad[threadIdx.x] = 1, a.res[15] = pad[(threadIdx.x + 1) % kThreads];
+#endif
   DevBlock bk{scratch};
   fsvm::tile<MODE>(a, sh, bk, blockIdx.x);
 }
