@@ -39,6 +39,7 @@ CONFIGS = {
     "libsvm_1m_x2048": ("libsvm", 1 << 20, 2048, 3),
     "libsvm_32m_x64": ("libsvm", 32 << 20, 64, 4),
     "libfm_1m_x64": ("libfm", 1 << 20, 64, None),  # SURVEY 8(f) row 3, not a BASELINE config
+    "libsvm_qid_1m_x128": ("libsvm_qid", 1 << 20, 128, None),  # config 2's rows with qid: (ranking data)
 }
 DESC = {
     "libsvm_1m_x128": "libsvm 1M rows x 128 nnz/row, device-resident",
@@ -46,7 +47,13 @@ DESC = {
     "libsvm_1m_x2048": "libsvm 1M rows x 2048 nnz/row, device-resident",
     "libsvm_32m_x64": "libsvm 32M rows x 64 nnz/row, chunks sharded across GPUs",
     "libfm_1m_x64": "libfm 1M rows x 64 field:id:value/row, device-resident",
+    "libsvm_qid_1m_x128": "libsvm 1M rows x 128 nnz/row with qid:<row/16> on every row, device-resident",
 }
+SYNTH = {"libsvm": synth.LIBSVM, "csv": synth.CSV, "libfm": synth.LIBFM, "libsvm_qid": synth.LIBSVM_QID}
+# the arithmetic the path computes in (values decoded to f32 through the
+# reference's f64 fraction divide; indices / fields as u32)
+DTYPE = {"libsvm": "f32 values / u32 index", "libsvm_qid": "f32 values / u32 index / u64 qid",
+         "csv": "f32 values", "libfm": "f32 values / u32 index / u32 field"}
 
 
 def log(*a):
@@ -80,26 +87,36 @@ def hbm_copy_rate(dev, nbytes=4 << 30, reps=5):
     return round(2 * nbytes / best / 1e9, 1)
 
 
-def cpu_baseline(text, starts, fmt, budget_s):
+def cpu_baseline(text, starts, fmt, budget_s, wide=False):
     """Reference CPU parser (oracle/_ref when it travelled here, else the C
-    restatement) over a bounded prefix of this shard's chunks."""
+    restatement) over a bounded prefix of this shard's chunks.
+
+    Thread model (oracle/ref_harness.cc ref_bench_blocks): T threads started
+    once, each parsing whole chunks round-robin with the format's ParseBlock;
+    T = the reference's factory cap min(max(nproc/2 - 4, 1), 2)
+    (text_parser.h:32-35, data.cc:31), or with wide=True the uncapped
+    max(nproc/2 - 4, 1); nproc = the CPUs this process may
+    run on (omp_get_num_procs)."""
     from oracle import pyoracle as po
     f = {"libsvm": po.LIBSVM, "csv": po.CSV, "libfm": po.LIBFM}[fmt]
-    nproc = os.cpu_count() or 1
+    nproc = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
     use_ref = po.ref_available()
-    # the reference's thread cap: min(max(nprocs/2 - 4, 1), nthread=2), text_parser.h:33-34, data.cc:31
-    nthread = min(max(nproc // 2 - 4, 1), 2) if use_ref else 1
-    # probe on 4 chunks, then size the sample to ~budget_s
-    k0 = min(4, len(starts) - 1)
+    nthread = max(nproc // 2 - 4, 1) if wide else min(max(nproc // 2 - 4, 1), 2)
+    if not use_ref:
+        nthread = 1
+    # probe on a few chunks per thread, then size the sample to ~budget_s
+    k0 = min(max(4, 2 * nthread), len(starts) - 1)
     t, _, _, _ = po.bench_chunks(text, starts[:k0 + 1], f, nthread, use_ref)
     per_chunk = t / max(k0, 1)
     k = int(min(len(starts) - 1, max(k0, budget_s / max(per_chunk, 1e-9))))
     secs, nnz, kind, thr = po.bench_chunks(text, starts[:k + 1], f, nthread, use_ref)
     nb = int(starts[k])
     return {"value": round(nb / secs / 1e9, 4), "unit": "GB/s", "cores": thr, "kind": kind,
-            "sample": "%d of %d InputSplit chunks (%.1f MB, %d nnz) of the same shard, "
-                      "ParseBlock per chunk, %d thread(s) (reference cap min(max(nproc/2-4,1),2), "
-                      "nproc=%d), %.1f s" % (k, len(starts) - 1, nb / 1e6, nnz, thr, nproc, secs)}
+            "sample": "%d of %d InputSplit chunks (%.1f MB, %d nnz) of the same shard, %d thread(s) "
+                      "each parsing whole chunks round-robin with ParseBlock (%s, nproc=%d), %.1f s"
+                      % (k, len(starts) - 1, nb / 1e6, nnz, thr,
+                         "uncapped max(nproc/2-4,1)" if wide else "reference cap min(max(nproc/2-4,1),2)",
+                         nproc, secs)}
 
 
 def main():
@@ -140,8 +157,7 @@ def main():
     if args.rows:
         rows = args.rows
     t0 = time.time()
-    text, _ = synth.rows({"libsvm": synth.LIBSVM, "csv": synth.CSV, "libfm": synth.LIBFM}[fmt], rows, width, seed=1,
-                         row0=rank * rows)
+    text, _ = synth.rows(SYNTH[fmt], rows, width, seed=1, row0=rank * rows)
     starts = dmlc_amd.text_chunk_starts(text)
     log("[rank %d] generated %s: %d rows, %.3f GB, %d chunks in %.1f s"
         % (rank, args.config, rows, text.size / 1e9, len(starts) - 1, time.time() - t0))
@@ -150,7 +166,8 @@ def main():
     d_starts = torch.from_numpy(starts).to(dev)
     nbytes = int(text.size)
     pkw = {"label_column": args.label_column} if fmt == "csv" else {}
-    p = dmlc_amd.DeviceParser(fmt, tile_bytes=args.tile_bytes, **pkw)
+    pfmt = "libsvm" if fmt == "libsvm_qid" else fmt
+    p = dmlc_amd.DeviceParser(pfmt, tile_bytes=args.tile_bytes, **pkw)
     res = torch.zeros(16, dtype=torch.int64, device=dev)
     counts = p.count(d_text, d_starts, result=res)
     out = p.alloc(counts)
@@ -172,7 +189,10 @@ def main():
         raise RuntimeError("parse error %#x" % int(r[8]))
     if [int(x) for x in r[:7]] != [int(x) for x in counts[:7]]:
         raise RuntimeError("count mismatch between calls")
-    path = "exact tile kernels" if int(r[9]) else "single-pass uniform-grammar kernel"
+    gate = int(r[9])
+    if gate & 2:  # the look-back's safety valve handed the input to the exact kernels: not a valid fast-path number
+        raise RuntimeError("look-back valve fired (result.path %d)" % gate)
+    path = "exact tile kernels" if gate else "single-pass uniform-grammar kernel"
 
     if dist:
         dist.barrier()
@@ -194,6 +214,8 @@ def main():
     r = res.cpu().numpy().view(np.uint64)
     if int(r[8]) != 0:
         raise RuntimeError("parse error %#x" % int(r[8]))
+    if int(r[9]) != gate:
+        raise RuntimeError("path changed inside the timed region (%d -> %d)" % (gate, int(r[9])))
 
     ms_per_step = elapsed * 1e3 / args.steps
     total_in = nbytes * world
@@ -220,7 +242,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "u8",
+        "dtype": DTYPE[fmt],
         "data": "synthetic (tools/synth.c splitmix64 seed 1, %.9g values), HBM-resident",
         "config": {"workload": DESC[args.config], "baseline_config": cfg_idx, "format": fmt,
                    "rows_per_gpu": rows, "width": width, "input_bytes_per_gpu": nbytes,
@@ -244,7 +266,9 @@ def main():
             line["hbm_copy"] = {"error": repr(e)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            line["cpu_baseline"] = cpu_baseline(text, starts, fmt, args.cpu_budget)
+            line["cpu_baseline"] = cpu_baseline(text, starts, pfmt, args.cpu_budget)
+            if line["cpu_baseline"].get("kind") == "reference":
+                line["cpu_baseline_max_threads"] = cpu_baseline(text, starts, pfmt, args.cpu_budget / 2, wide=True)
         except Exception as e:  # reported, never fatal for the GPU number
             line["cpu_baseline"] = {"error": repr(e)}
     if rank == 0:

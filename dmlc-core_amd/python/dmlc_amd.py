@@ -19,6 +19,7 @@ ROWS, INDEX, VALUE, WEIGHT, QID, LABEL, FIELD = range(7)
 FLAG_COUNT_ONLY = 1
 FLAG_FILL_ONLY = 2
 FLAG_EXACT = 4
+FLAG_MAX_INDEX = 8  # result.max_index / max_field (RowBlockContainer::max_index, NumCol)
 ERR_CAPACITY = 16
 _FMT = {"libsvm": LIBSVM, "csv": CSV, "libfm": LIBFM}
 _VT = {"f32": F32, "float32": F32, "i32": I32, "int32": I32, "i64": I64, "int64": I64}
@@ -235,6 +236,7 @@ class DeviceParser:
         out["error"] = int(r[8])
         out["path"] = int(r[9])
         out["result_counts"] = [int(x) for x in r[:8]]
+        out["max_index"], out["max_field"] = int(r[10]), int(r[11])
         return out
 
 

@@ -335,8 +335,13 @@ float ref_parse_float(const char *s, size_t *consumed) {
   return v;
 }
 
-// Pure ParseBlock throughput over pre-loaded line-aligned chunks, `nthread`
-// std::threads each parsing whole chunks (bench.py cpu_baseline).
+// Pure ParseBlock throughput over pre-loaded line-aligned chunks (bench.py
+// cpu_baseline).  Thread model: `nthread` std::threads started once, thread t
+// parsing whole chunks t, t + nthread, ... with the format's own ParseBlock
+// (LibSVMParser / CSVParser / LibFMParser).  That is the reference's total
+// parse work at `nthread`-way parallelism; it is not FillData's per-chunk
+// split into nthread ranges with an OpenMP fork/join per chunk, whose
+// overhead it leaves out (an upper bound on the reference's rate).
 double ref_bench_blocks(const char *buf, const uint64_t *off, int nchunks, int format, int nthread,
                         uint64_t *nnz_out) {
   std::map<std::string, std::string> a;
@@ -348,11 +353,14 @@ double ref_bench_blocks(const char *buf, const uint64_t *off, int nchunks, int f
       RowBlockContainer<uint32_t, float> c;
       std::unique_ptr<SvmSeam<uint32_t, float>> svm;
       std::unique_ptr<CsvSeam<uint32_t, float>> csv;
+      std::unique_ptr<FmSeam<uint32_t, float>> fm;
       if (format == DMO_FMT_CSV) csv.reset(new CsvSeam<uint32_t, float>(a, 1));
+      else if (format == DMO_FMT_LIBFM) fm.reset(new FmSeam<uint32_t, float>(a, 1));
       else svm.reset(new SvmSeam<uint32_t, float>(a, 1));
       for (int k = t; k < nchunks; k += nthread) {
         const char *b = buf + off[k], *e = buf + off[k + 1];
         if (csv) csv->Call(b, e, &c);
+        else if (fm) fm->Call(b, e, &c);
         else svm->Call(b, e, &c);
         nnz[t] += c.index.size();
       }

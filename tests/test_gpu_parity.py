@@ -382,6 +382,103 @@ def test_gpu_sharded_parts_concat(dm):
                 assert np.asarray(cat[k]).tobytes() == np.asarray(whole[k]).tobytes(), (name, world, k)
 
 
+def test_gpu_config4_wide_rows_vs_oracle(dm):
+    """BASELINE config 4's rows (2048 nnz each, ~35 KiB: every row crosses
+    two or three 16 KiB tiles) at an oracle-checkable size: 6000 rows in 8 MiB
+    InputSplit chunks, nthread 1 and 2, both index widths."""
+    text, _ = synth.rows(synth.LIBSVM, 6000, 2048, seed=4)
+    data = text.tobytes()
+    offs = dm.text_chunk_starts(text, 8 << 20).tolist()
+    assert len(offs) > 20
+    for kw in ({}, {"nthread": 2}, {"index_bits": 64}):
+        o = po.parse_chunks(data, offs, fmt=po.LIBSVM, **kw)
+        h = dm.parse_bytes(data, offs, fmt="libsvm", **kw)
+        assert o["status"] == 0 and h["error"] == 0 and h["path"] == "fast", kw
+        assert diff(h, o) == [], kw
+        assert h["counts"][dm.INDEX] == 6000 * 2048
+
+
+def test_gpu_config4_full_size_fast_equals_exact(dm):
+    """Config 4 at full size (1M rows x 2048 nnz, ~37 GB of text): a 64k-row
+    block repeated 16 times on the device (the repeats shift the tile / row
+    alignment), single-pass kernel == exact kernels bit for bit, plus CSR
+    properties (2048 per row, strictly increasing ids, values in [0, 1))."""
+    import torch
+    blk, _ = synth.rows(synth.LIBSVM, 1 << 16, 2048, seed=1)
+    d_blk = torch.from_numpy(blk).cuda()
+    d_text = d_blk.repeat(16)
+    del d_blk
+    starts = dm.text_chunk_starts(blk)
+    reps = [torch.from_numpy(starts[:-1].astype(np.int64)) + r * blk.size for r in range(16)]
+    d_cs = torch.cat(reps + [torch.tensor([16 * blk.size])]).cuda()
+    outs = {}
+    for exact in (False, True):
+        p = dm.DeviceParser("libsvm", flags=dm.FLAG_EXACT if exact else 0)
+        out = p.parse(d_text, d_cs)
+        assert out["error"] == 0 and out["path"] == (1 if exact else 0)
+        outs[exact] = out
+    c = outs[False]["counts"]
+    assert c[:7] == outs[True]["counts"][:7]
+    assert c[dm.ROWS] == 1 << 20 and c[dm.INDEX] == 2048 << 20 and c[dm.VALUE] == 2048 << 20
+    for k in ("offset", "label", "index", "value"):
+        a, b = outs[False][k], outs[True][k]
+        assert torch.equal(a.view(torch.int32) if a.dtype == torch.float32 else a,
+                           b.view(torch.int32) if b.dtype == torch.float32 else b), k
+    del outs[True]
+    off = outs[False]["offset"]
+    assert bool((off[1:] - off[:-1] == 2048).all())
+    idx = outs[False]["index"].view(-1, 2048)
+    assert bool((idx[:, 1:].to(torch.int64) > idx[:, :-1].to(torch.int64)).all())
+    v = outs[False]["value"]
+    assert bool(((v >= 0) & (v < 1)).all())
+
+
+def test_gpu_max_index_flag(dm):
+    """FLAG_MAX_INDEX: result.max_index / max_field are the largest index and
+    field written (RowBlockContainer::max_index, BasicRowIter::NumCol - 1),
+    on the fast and the exact path, libsvm and libfm."""
+    import torch
+    for fmt, kind in (("libsvm", synth.LIBSVM), ("libfm", synth.LIBFM)):
+        text, _ = synth.rows(kind, 30000, 40, seed=12)
+        starts = dm.text_chunk_starts(text, 1 << 20)
+        d_text, d_cs = torch.from_numpy(text).cuda(), torch.from_numpy(starts).cuda()
+        for flags in (dm.FLAG_MAX_INDEX, dm.FLAG_MAX_INDEX | dm.FLAG_EXACT):
+            p = dm.DeviceParser(fmt, flags=flags)
+            out = p.parse(d_text, d_cs)
+            assert out["error"] == 0
+            n = out["counts"][dm.INDEX]
+            assert out["max_index"] == int(out["index"][:n].max())
+            if fmt == "libfm":
+                assert out["max_field"] == int(out["field"][:n].max())
+
+
+def test_gpu_config5_shards_vs_oracle(dm):
+    """BASELINE config 5's sharding (64-nnz rows, 8 parts): each part's byte
+    range (dmlc_amd_dist.part_range) is the oracle InputSplit's part k, each
+    part's GPU parse equals the oracle's parse of that part's chunks, and the
+    Push-style concatenation equals the oracle's parse of the whole file."""
+    import dmlc_amd_dist as dd
+    text, _ = synth.rows(synth.LIBSVM, 200000, 64, seed=5)
+    data = text.tobytes()
+    world = 8
+    whole = po.parse_chunks(data, dm.text_chunk_starts(text, 8 << 20).tolist(), fmt=po.LIBSVM)
+    assert whole["status"] == 0
+    parts = []
+    for r in range(world):
+        chunks = po.split_text([data], r, world, 8 << 20)
+        b, e = dd.part_range(data, r, world)
+        assert b"".join(chunks) == data[b:e], r
+        offs = np.concatenate([[0], np.cumsum([len(c) for c in chunks])]).tolist()
+        o = po.parse_chunks(b"".join(chunks), offs, fmt=po.LIBSVM)
+        h = dd.parse_part(data, r, world, fmt="libsvm", chunk_bytes=8 << 20)
+        assert o["status"] == 0 and h["error"] == 0 and h["path"] == "fast", r
+        assert diff(h, o) == [], r
+        parts.append(h)
+    cat = dd.concat_csr(parts)
+    for k in ("offset", "label", "index", "value"):
+        assert np.asarray(cat[k]).tobytes() == np.asarray(whole[k]).tobytes(), k
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("fmt", [po.LIBSVM, po.CSV])
 def test_gpu_fast_many_chunks_vs_oracle(dm, fmt):

@@ -367,3 +367,24 @@ def test_api_errors_raise_at_the_failing_block(tmp_path):
     for bad in ("0", "abc"):
         h = run_api(tmp_path, d2, env={"DMLC_AMD_BATCH_BYTES": bad})
         assert h["index"].tolist() == [3], bad
+
+
+@pytest.mark.gpu
+def test_api_multi_device_dispatch(tmp_path):
+    """DMLC_AMD_DEVICES: the batches of one parser dispatched over a device
+    list ("all", or a list naming devices, here the box's device several
+    times: every slot gets its own workers and streams) come back in input
+    order -- Parser blocks and RowBlockIter (NumCol) equal to the oracle's
+    whole parse; a device that does not exist raises."""
+    text, _ = synth.rows(synth.LIBSVM, 40000, 64, seed=14)
+    d, _ = _write(tmp_path / "md", [text.tobytes()])
+    o, _ = oracle_files([text.tobytes()])
+    for devs in ("all", "0", "0,0,0"):
+        env = {"DMLC_AMD_DEVICES": devs, "DMLC_AMD_BATCH_BYTES": str(1 << 20)}
+        h = run_api(tmp_path, d, env=env)
+        assert "error" not in h and diff(h, o) == [], devs
+        assert h["blocks"].tolist() == o["blocks"]["rows"].tolist(), devs
+        hi = run_api(tmp_path, d, iter_=True, env=env)
+        assert diff(hi, o) == [] and int(hi["meta"][2]) == int(o["index"].max()) + 1, devs
+    bad = run_api(tmp_path, d, env={"DMLC_AMD_DEVICES": "99"})
+    assert "no HIP device" in bad["error"]

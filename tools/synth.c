@@ -12,6 +12,8 @@
  *  CSV row: C values uniform [-1,1) (24-bit mantissa), "%.9g", ',' separated.
  *  libfm row: "<label>( <field>:<id>:<value>)*\n", the libsvm row's ids and
  *    values with a field in [0,32) per feature (libfm_parser.h:67-144).
+ *  libsvm+qid row (fmt 3): "<label> qid:<q>( <id>:<value>)*\n", the libsvm
+ *    row with q = row / 16 (ranking data, libsvm_parser.h:119-132).
  */
 #include <stdint.h>
 #include <stdio.h>
@@ -30,10 +32,11 @@ static inline uint64_t row_state(uint64_t seed, uint64_t r) {
   return s;
 }
 
-static size_t fmt_libsvm_row(char *o, uint64_t seed, uint64_t r, int K) {
+static size_t fmt_libsvm_row(char *o, uint64_t seed, uint64_t r, int K, int qid) {
   uint64_t s = row_state(seed, r);
   char *p = o;
   *p++ = (char)('0' + (sm64(&s) & 1));
+  if (qid) p += sprintf(p, " qid:%llu", (unsigned long long)(r >> 4));
   uint64_t id = 0;
   for (int j = 0; j < K; ++j) {
     uint64_t x = sm64(&s);
@@ -76,7 +79,7 @@ static size_t fmt_csv_row(char *o, uint64_t seed, uint64_t r, int C) {
 
 /* upper bound on the bytes of `nrows` rows */
 size_t synth_bound(int fmt, uint64_t nrows, int width) {
-  return fmt == 0 ? nrows * (size_t)(2 + width * 26)
+  return fmt == 0 || fmt == 3 ? nrows * (size_t)(2 + 26 + width * 26)
                   : fmt == 2 ? nrows * (size_t)(2 + width * 30) : nrows * (size_t)(width * 18 + 2);
 }
 
@@ -98,7 +101,7 @@ size_t synth_rows(int fmt, uint64_t row0, uint64_t nrows, int width, uint64_t se
     size_t n = 0;
     for (uint64_t r = r0; r < r1; ++r) {
       if (line_off) line_off[r] = n; /* block-relative; fixed below */
-      n += fmt == 0 ? fmt_libsvm_row(buf + n, seed, row0 + r, width)
+      n += fmt == 0 || fmt == 3 ? fmt_libsvm_row(buf + n, seed, row0 + r, width, fmt == 3)
                     : fmt == 2 ? fmt_libfm_row(buf + n, seed, row0 + r, width)
                                : fmt_csv_row(buf + n, seed, row0 + r, width);
     }
