@@ -62,12 +62,13 @@ struct FastSvmArgs {
   uint64_t *offset;
   float *label;
   float *weight;
+  uint64_t *qid;        // libsvm "qid:" ids, one per row (svm_fast.h qid_decide)
   void *index;
   void *field;          // libfm: one field id per index (IndexType); null for libsvm
   float *value;
   uint64_t cap[8];
   uint64_t *chunk_tab;  // may be null
-  uint64_t *lb;         // [ntiles][8] look-back records, zeroed per launch
+  uint64_t *lb;         // look-back records [5 ntiles] (status words zeroed per launch), qid counts [ntiles]
   uint32_t *gate;       // != 0: input left the grammar -> exact path
   unsigned long long *err;  // first error of this path
   uint64_t *res;        // dmlc_amd_result counts (written by the last tile)

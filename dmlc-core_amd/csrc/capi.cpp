@@ -233,6 +233,7 @@ int dmlc_amd_parse(const void *d_text, uint64_t nbytes, const uint64_t *d_chunk_
     f.offset = a.offset;
     f.label = a.label;
     f.weight = a.weight;
+    f.qid = a.qid;
     f.index = a.index;
     f.value = a.value;
     for (int i = 0; i < 8; ++i) f.cap[i] = out->cap[i];

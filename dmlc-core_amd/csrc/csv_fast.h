@@ -210,7 +210,7 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
     bad = (m.g & ~m.d & vmask) != 0;
     if (tid < 16 && t.tlo > 0) {
       uint32_t x;
-      memcpy(&x, sh.c.text + 4 * tid, 4);
+      memcpy(&x, sh.c.text + (kPre - kSegB) + 4 * tid, 4);
       const Nib b = classify_dword_lut(x, sh.cls);
       atomic_or_u64(&sh.md[0], (uint64_t)b.d << (4 * tid));
       atomic_or_u64(&sh.mn[0], (uint64_t)b.n << (4 * tid));

@@ -12,7 +12,9 @@ namespace fast {
 
 constexpr int kSegB = 64;                // bytes per thread (one 64-bit mask)
 constexpr int kTile = kThreads * kSegB;  // 16 KiB of text per tile
-constexpr int kPre = 64;                 // staged bytes before the tile (look-back)
+constexpr int kPre = 64;                 // staged bytes before the tile (the segment before it)
+// (staging 80 bytes before the tile instead -- 16 more for the qid token
+// checks -- cost 11 % on the 1M x 128 libsvm launch: those read global memory)
 constexpr int kPost = 128;               // staged bytes after it (runs crossing the end)
 constexpr int kStage = kPre + kTile + kPost;
 constexpr int kMaxCs = 32;               // chunk starts per tile the fast path accepts
@@ -140,13 +142,17 @@ DA_HD Masks classify64(const uint8_t *p) {
 // ---- byte classes by table lookup (the VALU-cheap form on MI355X: one SDWA
 // shift + one shift-or per byte, the lookup on the LDS pipe).  Entry planes:
 // byte 0 D digitchar, 1 G digit, 2 N newline, 3 C colon; blanks are 0; a byte
-// outside the grammar is G without D.
+// outside the grammar is G without D.  The letters of "qid:" (libsvm only,
+// libsvm_parser.h:119-132) are N and C together, which no other byte is:
+// svm_fast.h qid_clean turns them into blanks and the token's ':' into a
+// qid marker (N and C) or flags them.
 DA_HD uint32_t class_of(uint32_t b) {
   if (b - '0' < 10u) return 0x00000101u;
   if (b == '+' || b == '-' || b == '.' || b == 'e' || b == 'E') return 0x00000001u;
   if (b == '\n' || b == '\r') return 0x00010000u;
   if (b == ':') return 0x01000000u;
   if (b == ' ' || b == '\t') return 0u;
+  if (b == 'q' || b == 'i' || b == 'd') return 0x01010000u;
   return 0x00000100u;
 }
 

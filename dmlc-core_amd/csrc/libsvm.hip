@@ -47,6 +47,30 @@ __global__ void reopen_kernel(uint64_t *res, uint64_t *offset, uint64_t cap_rows
   if (offset && res[0] < cap_rows + 1) offset[res[0]] = res[1];
 }
 
+// after the single-pass kernel: the tiles' qid run counts against the rows
+// (svm_fast.h qid_decide); when every row has a qid, each chunk row's qid
+// count is its row count
+__global__ void __launch_bounds__(256) qid_fix_kernel(const uint64_t *qcnt, uint32_t ntiles, uint64_t *res,
+                                                      uint32_t *gate, uint64_t *chunk_tab, int nchunk) {
+  __shared__ uint64_t part[256];
+  __shared__ int fix_tab;
+  uint64_t sum = 0;
+  for (uint32_t i = threadIdx.x; i < ntiles; i += 256) sum += qcnt[i];
+  part[threadIdx.x] = sum;
+  __syncthreads();
+  for (int d = 128; d > 0; d >>= 1) {
+    if ((int)threadIdx.x < d) part[threadIdx.x] += part[threadIdx.x + d];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) fix_tab = fsvm::qid_decide(part[0], res, gate) && chunk_tab;
+  __syncthreads();
+  if (fix_tab)
+    for (int i = threadIdx.x; i < nchunk; i += 256) {
+      uint64_t *row = chunk_tab + (uint64_t)i * 8;
+      if (row[C_ROWS] != ~0ull) row[C_QID] = row[C_ROWS];
+    }
+}
+
 // the error of whichever path produced the result
 __global__ void select_kernel(uint64_t *res, const uint32_t *gate, const unsigned long long *ferr) {
   if (*gate == 0) res[8] = *ferr;
@@ -83,6 +107,8 @@ hipError_t launch_libsvm(const LibsvmArgs &a, const FastSvmArgs &f, bool use_fas
       svm_fast_tile<2><<<f.ntiles, kThreads, 0, s>>>(f);
       prof_mark(1, s, "svm_fast_tile<2>");
     }
+    qid_fix_kernel<<<1, 256, 0, s>>>(f.lb + 5 * (uint64_t)f.ntiles, f.ntiles, res, gate,
+                                     phase != kPhaseCount ? f.chunk_tab : nullptr, f.nchunk);
   } else if ((e = hipMemsetAsync(f.err, 0xFF, sizeof(uint64_t), s)) != hipSuccess) {
     return e;
   }

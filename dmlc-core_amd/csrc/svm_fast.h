@@ -29,7 +29,55 @@ namespace dmlc_amd {
 namespace fsvm {
 using namespace fast;
 
-enum : uint32_t { R_NONE = 0, R_L = 1, R_K = 2, R_I = 3 };
+enum : uint32_t { R_NONE = 0, R_L = 1, R_K = 2, R_I = 3, R_Q = 4 };
+
+// After the single-pass kernel (qid_fix_kernel, and the emulator): its qid
+// runs stand only when every row has one -- qid[r] is then row r's and each
+// chunk's qid count its row count; a mix of rows with and without a qid goes
+// to the exact kernels.  Returns true when the chunk rows' qid counts must be
+// set to their row counts.
+DA_HD bool qid_decide(uint64_t total, uint64_t *res, uint32_t *gate) {
+  if (*gate || total == 0) return false;
+  if (total != res[C_ROWS]) {
+    *gate |= 1u;
+    return false;
+  }
+  res[C_QID] = total;
+  return true;
+}
+
+// ---- "qid:<n>" (libsvm_parser.h:119-132) in the fast grammar.  The letters
+// q, i, d classify as N and C together (fast_common.h class_of); qid_clean
+// makes them blanks and the token's ':' a qid marker (N and C together), so
+// the gap in front of a qid run carries a marker the role arithmetic sees
+// like it sees a newline or a ':'.  Bytes [P, P + 64) with raw planes n, c;
+// lead: the byte at P - 1 is a letter; at(p): the byte at p (0 outside the
+// text).  Returns false on a letter outside a token or a token not followed
+// by a digit (atoll's digits).
+DA_HD bool is_qid_letter(uint32_t b) { return b == 'q' || b == 'i' || b == 'd'; }
+// (inline: out of line, the call's stack frame cost the kernel 2.3x)
+template <class At>
+DA_HD bool qid_clean(uint64_t P, uint64_t *n, uint64_t *c, bool lead, At at) {
+  const uint64_t X = *n & *c;
+  bool ok = true;
+  for (uint64_t m = X; m; m &= m - 1) {
+    const uint64_t x = P + ctz64(m);
+    const uint32_t b = at(x);
+    const uint64_t s0 = x - (b == 'q' ? 0u : b == 'i' ? 1u : 2u);
+    ok = ok && at(s0) == 'q' && at(s0 + 1) == 'i' && at(s0 + 2) == 'd' && at(s0 + 3) == ':';
+  }
+  uint64_t qc = 0;
+  for (uint64_t m = *c & ~X & ((X << 1) | (lead ? 1u : 0u)); m; m &= m - 1) {
+    const uint64_t x = P + ctz64(m);
+    if (at(x - 1) == 'd' && at(x - 2) == 'i' && at(x - 3) == 'q') {
+      qc |= m & (0 - m);
+      ok = ok && is_digit(at(x + 1));
+    }
+  }
+  *n = (*n & ~X) | qc;
+  *c &= ~X;
+  return ok;
+}
 
 // look-back counter slots (record words 0-3: aggregate, 4-7: inclusive prefix)
 enum { Q_ROWS = 0, Q_INDEX = 1, Q_VALUE = 2, Q_WEIGHT = 3 };
@@ -57,6 +105,7 @@ struct Shared {  // LDS of one workgroup
   uint32_t gw[2 * kThreads + 2];  // digit plane as words: 2t, 2t+1 segment t; 2 kThreads: the post-halo
   uint64_t pend[kTile / kPassRuns + 2];  // packed inclusive counts at the end of each pass
   uint32_t npass;
+  uint32_t nq;  // qid runs of the tile
 };
 
 struct Tile {
@@ -82,7 +131,9 @@ struct Tile {
     for (int i = 0; i < 64; ++i) {
       const uint32_t b = p[i];
       md |= (uint64_t)is_digitchar(b) << i;
-      mn |= (uint64_t)is_nl(b) << i;
+      // a qid token's ':' is a marker (N and C), its letters blanks (qid_clean)
+      const bool qm = b == ':' && (g << 6) + i >= 3 && p[i - 1] == 'd' && p[i - 2] == 'i' && p[i - 3] == 'q';
+      mn |= (uint64_t)(is_nl(b) || qm) << i;
       mc |= (uint64_t)(b == ':') << i;
     }
     *d = md;
@@ -91,13 +142,13 @@ struct Tile {
   }
 
   // last position in [lo, hi) whose bit is set in mask `kind` (0 D, 1 not-D,
-  // 2 newline, 3 colon), or kNone
+  // 2 newline, 3 colon, 4 qid marker), or kNone
   DA_HD uint64_t last_bit(int kind, uint64_t lo, uint64_t hi) const {
     if (lo >= hi) return kNone;
     for (uint64_t g = (hi - 1) >> 6;; --g) {
       uint64_t d, n, c;
       seg(g, &d, &n, &c);
-      uint64_t w = kind == 0 ? d : kind == 1 ? ~d : kind == 2 ? n : c;
+      uint64_t w = kind == 0 ? d : kind == 1 ? ~d : kind == 2 ? n & ~c : kind == 3 ? c & ~n : n & c;
       const uint64_t b0 = g << 6;
       if (hi - b0 < 64) w &= (1ull << (hi - b0)) - 1;
       if (lo > b0) w &= ~((1ull << (lo - b0)) - 1);
@@ -128,8 +179,48 @@ struct Tile {
     const uint64_t p = last_bit(0, f, q);
     if (p == kNone) return R_L;
     if (last_bit(2, p + 1, q) != kNone) return R_L;
+    if (last_bit(4, p + 1, q) != kNone) return R_Q;
     if (last_bit(3, p + 1, q) != kNone) return R_K;
     return R_I;
+  }
+
+  // The qid run at x (its token "qid:" at x - 4) stands where the reference
+  // reads one: right after the line's label -- ParsePair skipped the blanks
+  // after it (strtonum.h:667-703) -- or after label:weight with spaces only
+  // in between (libsvm_parser.h:119-124); and it is 1-18 plain digits
+  // (atoll, then the digitchar skip, :126-129).  Reads the staged text; a
+  // line reaching back before it reads as not ok (the exact kernels decide).
+  DA_HD bool qid_ok(uint64_t x) const {
+    const uint8_t *txt = sh->c.text;
+    const uint64_t base = tlo;
+    auto at = [&](uint64_t p) -> uint32_t { return txt[p - base + kPre]; };
+    uint32_t len = 0;
+    while (len < 19 && is_digit(at(x + len))) ++len;
+    if (len > 18 || is_digitchar(at(x + len))) return false;
+    const uint64_t F = floor_of(x);
+    const uint64_t lo = tlo >= (uint64_t)kPre ? tlo - kPre : 0;
+    const uint64_t lim = F > lo ? F : lo;  // bytes before it are another line's, or not staged
+    if (x < lim + 5) return false;
+    uint64_t e = x - 4;  // the scan examines byte e - 1
+    bool tab = false;
+    while (e > lim && is_blank(at(e - 1))) tab |= at(--e) == '\t';
+    if (e == lim || !is_digitchar(at(e - 1))) return false;  // no run before the token
+    while (e > lim && is_digitchar(at(e - 1))) --e;
+    if (e == F) return true;  // the line's label
+    while (e > lim && is_blank(at(e - 1))) --e;
+    if (e == F) return true;
+    if (e == lim) return false;
+    const uint32_t g = at(e - 1);
+    if (is_nl(g)) return true;          // the line's label
+    if (g != ':' || tab) return false;  // not label:weight, or a tab after the weight
+    --e;
+    while (e > lim && is_blank(at(e - 1))) --e;
+    if (e == lim || !is_digitchar(at(e - 1))) return false;
+    while (e > lim && is_digitchar(at(e - 1))) --e;
+    if (e == F) return true;
+    while (e > lim && is_blank(at(e - 1))) --e;
+    if (e == F) return true;
+    return e > lim && is_nl(at(e - 1));
   }
 };
 
@@ -137,15 +228,16 @@ struct Tile {
 // (bit i <-> P-64+i), when no chunk starts in (P-64, P] and the previous run
 // and its gap lie inside those 64 bytes (the common case).  Returns false
 // when the general look-back (Tile::last_bit) is needed.
-DA_HD bool carry_fast(uint64_t d1, uint64_t n1, uint64_t c1, uint32_t *dc, uint32_t *ginl,
-                      uint32_t *ginc, uint32_t *prole) {
+DA_HD bool carry_fast(uint64_t d1, uint64_t n1r, uint64_t c1r, uint32_t *dc, uint32_t *ginl, uint32_t *ginc,
+                      uint32_t *ginq, uint32_t *prole) {
+  const uint64_t n1 = n1r & ~c1r, c1 = c1r & ~n1r, q1 = n1r & c1r;  // newline, ':', qid marker
   *dc = (uint32_t)(d1 >> 63);
   uint32_t qb;  // first bit of the last run that starts before P
   if (*dc) {
     const uint64_t nd = ~d1;
     if (!nd) return false;
     qb = 64 - clz64(nd);
-    *ginl = *ginc = 0;
+    *ginl = *ginc = *ginq = 0;
   } else {
     if (!d1) return false;
     const uint32_t pb = 63 - clz64(d1);  // last digitchar, <= 62
@@ -155,6 +247,7 @@ DA_HD bool carry_fast(uint64_t d1, uint64_t n1, uint64_t c1, uint32_t *dc, uint3
     const uint32_t ln = tgn ? 63 - clz64(tgn) : 0;
     const uint64_t after = !tgn ? tg : (ln == 63 ? 0ull : ~0ull << (ln + 1));
     *ginc = (c1 & after) != 0;
+    *ginq = (q1 & after) != 0;
     const uint64_t nd = ~d1 & ((1ull << pb) - 1);
     if (!nd) return false;
     qb = 64 - clz64(nd);
@@ -164,37 +257,38 @@ DA_HD bool carry_fast(uint64_t d1, uint64_t n1, uint64_t c1, uint32_t *dc, uint3
   if (!below) return false;
   const uint32_t p2 = 63 - clz64(below);
   const uint64_t gm = ((1ull << qb) - 1) & ~((2ull << p2) - 1);
-  *prole = (n1 & gm) ? R_L : ((c1 & gm) ? R_K : R_I);
+  *prole = (n1 & gm) ? R_L : (q1 & gm) ? R_Q : ((c1 & gm) ? R_K : R_I);
   return true;
 }
 
 // Runs, roles and counts of segment tid (positions P .. P+63).
 struct SegOut {
-  uint64_t L, W, I, V;
+  uint64_t L, W, I, V, Q;
   uint32_t bad;
 };
 
 DA_HD SegOut segment_roles(const Tile &t, int tid) {
   SegOut o;
-  o.L = o.W = o.I = o.V = 0;
+  o.L = o.W = o.I = o.V = o.Q = 0;
   o.bad = 0;
   const FastSvmArgs &a = *t.a;
   const uint64_t P = t.tlo + (uint64_t)tid * kSegB;
   if (P >= a.n) return o;
   const int nv = (int)mn<uint64_t>(64, a.n - P);
   const uint64_t valid = nv == 64 ? ~0ull : ((1ull << nv) - 1);
-  const uint64_t D = t.sh->u.m.d[tid + 1], N = t.sh->u.m.n[tid + 1], C = t.sh->u.m.c[tid + 1];
+  const uint64_t D = t.sh->u.m.d[tid + 1], Nr = t.sh->u.m.n[tid + 1], Cr = t.sh->u.m.c[tid + 1];
+  const uint64_t N = Nr & ~Cr, C = Cr & ~Nr, QM = Nr & Cr;  // newline, ':', qid marker
   uint64_t S = 0;
   for (uint32_t i = 0; i < t.sh->c.ncs; ++i) {
     const uint64_t x = t.sh->c.csl[i];
     if (x >= P && x < P + (uint64_t)nv) S |= 1ull << (x - P);
   }
   // ---- carry-in: state just before P
-  uint32_t dc = 0, ginl = 0, ginc = 0, prole = R_NONE;
+  uint32_t dc = 0, ginl = 0, ginc = 0, ginq = 0, prole = R_NONE;
   const uint64_t F = t.floor_of(P);
-  if (P != F && !(F + 64 <= P &&
-                  carry_fast(t.sh->u.m.d[tid], t.sh->u.m.n[tid], t.sh->u.m.c[tid], &dc, &ginl, &ginc, &prole))) {
-    dc = ginl = ginc = 0;
+  if (P != F && !(F + 64 <= P && carry_fast(t.sh->u.m.d[tid], t.sh->u.m.n[tid], t.sh->u.m.c[tid], &dc, &ginl,
+                                            &ginc, &ginq, &prole))) {
+    dc = ginl = ginc = ginq = 0;
     prole = R_NONE;
     uint64_t d, n, c;
     t.seg((P - 1) >> 6, &d, &n, &c);
@@ -210,6 +304,7 @@ DA_HD SegOut segment_roles(const Tile &t, int tid) {
         const uint64_t ln = t.last_bit(2, p + 1, P);
         ginl = ln != kNone;
         ginc = t.last_bit(3, ginl ? ln + 1 : p + 1, P) != kNone;
+        ginq = t.last_bit(4, ginl ? ln + 1 : p + 1, P) != kNone;
         const uint64_t x = t.last_bit(1, F, p);
         prole = t.role_of(x == kNone ? F : x + 1, F);
       }
@@ -229,15 +324,29 @@ DA_HD SegOut segment_roles(const Tile &t, int tid) {
   if (t2 & (NS | ~valid)) o.bad = 1;
   if (co && (P + 64 >= a.n || t.is_cs(P + 64))) o.bad = 1;
   const uint64_t K = RS & t2 & ~L;
+  uint64_t Q = 0;
+  if (QM | ginq) {  // qid runs: the gap in front holds a qid marker
+    uint32_t cq;
+    const uint64_t t3 = add_carry(G2, QM & G2, ginq, &cq);
+    if (t3 & (NS | ~valid)) o.bad = 1;
+    if (cq && (P + 64 >= a.n || t.is_cs(P + 64))) o.bad = 1;
+    Q = RS & t3 & ~L;
+    if (Q & K) o.bad = 1;  // a ':' and a token in one gap ("l : qid:5" pairs l with 5)
+    for (uint64_t m = Q; m; m &= m - 1)
+      if (!t.qid_ok(P + ctz64(m))) o.bad = 1;
+  }
   const uint64_t Z = ~RS;
-  const uint64_t xl = L << 1, xk = K << 1;
+  const uint64_t xl = L << 1, xk = K << 1, xq = Q << 1;
   const uint64_t prevL = ((Z + (xl & Z) + (prole == R_L ? 1u : 0u)) | xl) & RS;
   const uint64_t prevK = ((Z + (xk & Z) + (prole == R_K ? 1u : 0u)) | xk) & RS;
+  const uint64_t prevQ = ((Z + (xq & Z) + (prole == R_Q ? 1u : 0u)) | xq) & RS;
   if (K & prevK) o.bad = 1;  // "a:b:c": the pair grammar re-pairs (strtonum.h:684-702)
+  if (K & prevQ) o.bad = 1;  // "qid:5:x": the digitchar skip stops at the ':' (libsvm_parser.h:127-129)
   o.L = L;
   o.W = K & prevL;
   o.V = K & ~prevL;
-  o.I = RS & ~L & ~K;
+  o.Q = Q;
+  o.I = RS & ~L & ~K & ~Q;
   return o;
 }
 
@@ -399,7 +508,10 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
   stage_issue(a.text, a.n, t.tlo, sr, bk);  // text loads first: the chunk search overlaps them
   ChunkProbe cp;  // wave 0: the window load stays in flight through classification
   if (tid < kWave) cp = chunk_list_begin(a.cs, a.nchunk, t.tlo, bk);
-  if (tid == 0) sh.u.m.d[0] = sh.u.m.n[0] = sh.u.m.c[0] = 0;
+  if (tid == 0) {
+    sh.u.m.d[0] = sh.u.m.n[0] = sh.u.m.c[0] = 0;
+    sh.nq = 0;
+  }
   sh.cls[tid] = class_of((uint32_t)tid);
   init_dec_tables(sh.dt, bk);
   stage_commit(a.text, a.n, t.tlo, sr, sh.c, bk);
@@ -412,8 +524,18 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
   // ---- classify: segment tid -> slot tid+1; lanes 0..15 also one word each
   // of the 64 bytes before the tile -> slot 0
   uint32_t bad = 0;
+  // a text byte (0 outside the text) for the qid token checks: staged, or
+  // from global memory before the staged bytes
+  auto at = [&](uint64_t p) -> uint32_t {
+    if (p >= a.n) return 0u;
+    return p + kPre >= t.tlo ? (uint32_t)sh.c.text[p - t.tlo + kPre] : (uint32_t)a.text[p];
+  };
   {
-    const Masks m = classify64_lut(sh.c.text + kPre + tid * kSegB, sh.cls);
+    Masks m = classify64_lut(sh.c.text + kPre + tid * kSegB, sh.cls);
+    const uint64_t P0 = t.tlo + (uint64_t)tid * kSegB;
+    if ((m.n & m.c) || ((m.c & 1) && P0 > 0 && is_qid_letter(at(P0 - 1)))) {  // letters: "qid:" tokens
+      if (FM || !qid_clean(P0, &m.n, &m.c, P0 > 0 && is_qid_letter(at(P0 - 1)), at)) bad = 1;
+    }
     sh.gw[2 * tid] = (uint32_t)m.g;
     sh.gw[2 * tid + 1] = (uint32_t)(m.g >> 32);
     if (tid == kWave) {  // digits of the 16 bytes after the tile (windows of my last runs)
@@ -432,11 +554,17 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
     bad = m.bad;
     if (tid < 16 && t.tlo > 0) {
       uint32_t x;
-      memcpy(&x, sh.c.text + 4 * tid, 4);
+      memcpy(&x, sh.c.text + (kPre - kSegB) + 4 * tid, 4);
       const Nib b = classify_dword_lut(x, sh.cls);
+      uint64_t bn = b.n, bc = b.c;
+      const uint64_t P0 = t.tlo - kSegB + 4 * tid;
+      if (!FM && ((bn & bc) || (bc & 1))) {  // the bytes' owner tile checks them; here only their planes
+        const bool lead = is_qid_letter(at(P0 - 1));
+        if ((bn & bc) || lead) (void)qid_clean(P0, &bn, &bc, lead, at);
+      }
       atomic_or_u64(&sh.u.m.d[0], (uint64_t)b.d << (4 * tid));
-      atomic_or_u64(&sh.u.m.n[0], (uint64_t)b.n << (4 * tid));
-      atomic_or_u64(&sh.u.m.c[0], (uint64_t)b.c << (4 * tid));
+      atomic_or_u64(&sh.u.m.n[0], bn << (4 * tid));
+      atomic_or_u64(&sh.u.m.c[0], bc << (4 * tid));
     }
   }
   if (tid < kWave) chunk_list_end(a.cs, a.nchunk, t.tlo, t.thi, cp, sh.c, bk);
@@ -460,6 +588,7 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
     soF = sf.F;
   } else {
     so = segment_roles(t, tid);
+    if (so.Q) atomic_add_u32(&sh.nq, (uint32_t)popc64(so.Q));
   }
   if (so.bad | bad) atomic_or_u32(&sh.c.bad, 1u);
   // per-thread role counts packed in 16-bit fields (a tile holds < 2^16 runs)
@@ -479,6 +608,7 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
   if (tid == 0) {
     publish_aggregate(a.lb, a.ntiles, k, cnt4);
     if (sh.c.bad) atomic_or_u32(a.gate, 1u);
+    if (!FM) a.lb[5 * (uint64_t)a.ntiles + k] = sh.nq;  // qid_fix_kernel's per-tile qid counts
   }
   const uint64_t P = t.tlo + (uint64_t)tid * kSegB;
   const bool one_chunk = sh.c.ncs == 0;  // no chunk boundary before cnext
@@ -740,6 +870,16 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
       const uint64_t below = (m & (0 - m)) - 1;
       if (rl < a.cap[C_ROWS]) a.offset[rl] = eI + popc64(so.I & below);
       else raise_error(a.err, E_CAPACITY, P + ctz64(m));
+    }
+    // qid runs (every row has one when this path stands, qid_fix_kernel):
+    // row r's id, atoll of its digits (libsvm_parser.h:126-130)
+    for (uint64_t m = so.Q; m; m &= m - 1) {
+      const uint64_t bit = m & (0 - m), x = P + ctz64(m);
+      const uint64_t r = eL + popc64(so.L & (bit - 1)) - 1;  // the row of the label before it
+      uint64_t v = 0;
+      for (uint64_t p = x; is_digit(at(p)); ++p) v = v * 10 + (at(p) - '0');
+      if (r < a.cap[C_QID]) a.qid[r] = v;
+      else raise_error(a.err, E_CAPACITY, x);
     }
   } else {
     // libfm: the register batch, then the rest of this segment's runs, one

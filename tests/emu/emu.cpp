@@ -236,6 +236,7 @@ extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *c
       f.offset = a.offset;
       f.label = a.label;
       f.weight = a.weight;
+      f.qid = a.qid;
       f.index = a.index;
       f.field = fm ? out->field : nullptr;
       f.value = a.value;
@@ -258,6 +259,13 @@ extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *c
           }
         });
         delete sh;
+      }
+      if (!fm) {  // qid_fix_kernel (libsvm.hip)
+        uint64_t total = 0;
+        for (uint64_t k = 0; k < nft; ++k) total += lb[5 * nft + k];
+        if (fsvm::qid_decide(total, res, &gate) && chunk_table && !count_only)
+          for (int i = 0; i < nchunks; ++i)
+            if (chunk_table[i * 8 + C_ROWS] != ~0ull) chunk_table[i * 8 + C_QID] = chunk_table[i * 8 + C_ROWS];
       }
     }
     if (gate) {

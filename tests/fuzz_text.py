@@ -73,6 +73,40 @@ def uniform_libsvm(rng, nlines, maxfeat=40, violate=False):
     return text.encode("latin-1")
 
 
+def qid_libsvm(rng, nlines, maxfeat=40, violate=False, mixed=False):
+    """libsvm ranking rows, "<label>[:<weight>] qid:<n> <idx>:<val> ...", in the
+    fast grammar (svm_fast.h qid_clean / qid_ok): the token after the label
+    (any blanks) or after label:weight (spaces), 1-18 digits.  violate=True
+    mixes in the forms the reference reads differently (a tab after the
+    weight, "qid: 5", "qid:5.5", a second token, a token among the features,
+    19 digits, stray letters); mixed=True leaves some rows without a qid."""
+    out = []
+    for _ in range(nlines):
+        if rng.random() < 0.03:
+            out.append("")
+            continue
+        parts = [_num(rng) if rng.random() < 0.3 else str(int(rng.integers(0, 5)))]
+        wt = rng.random() < 0.25
+        if wt:
+            parts.append(rng.choice([":", " :", ": "]) + _num(rng))
+        q = str(int(rng.integers(0, 10 ** int(rng.integers(1, 19)))))
+        sep = rng.choice([" ", "  ", " ", ""] if wt else [" ", "\t", "  ", " \t", ""])
+        tok = sep + "qid:" + q
+        if violate and rng.random() < 0.15:
+            tok = rng.choice(["\tqid:" + q if wt else " qid: " + q, " qid:5.5", " qid:-3", " qid:", " qid:5:3",
+                              " QID:1", " qidd:1", " qid:1 qid:2", " qid:" + "9" * 19, " iqd:4", " q"])
+        if not (mixed and rng.random() < 0.1):
+            parts.append(tok)
+        for j in range(int(rng.integers(0, maxfeat + 1))):
+            parts.append(_blank(rng) + _idx(rng) + ":" + _num(rng))
+            if violate and rng.random() < 0.01:
+                parts.append(" qid:7")
+        out.append("".join(parts))
+    seps = ["\n"] * 12 + ["\r\n", "\r"]
+    text = "".join(line + seps[int(rng.integers(0, len(seps)))] for line in out)
+    return text.encode("latin-1")
+
+
 def dense_libsvm(rng, nbytes, style):
     """libsvm text with the shortest runs the grammar allows, so a 16 KiB tile
     holds several thousand runs (the fast kernel's run lists then take

@@ -169,6 +169,26 @@ def test_emu_fast_dense_runs():
         assert h["path"] == "fast", style
 
 
+def test_emu_fast_qid_vs_oracle():
+    """"qid:" in the single-pass grammar (svm_fast.h qid_clean / qid_ok /
+    qid_decide): ranking rows, one and several tiles, odd chunkings; the
+    forms the reference reads differently and rows without a qid go to the
+    exact kernels -- whichever path runs, the reference's result."""
+    rng = np.random.default_rng(4242)
+    paths = {"fast": 0, "exact": 0}
+    for it in range(40):
+        big = it % 8 == 0
+        data = fuzz_text.qid_libsvm(rng, 400 if big else int(rng.integers(1, 30)), 40 if big else 12,
+                                    violate=it % 4 == 3, mixed=it % 10 == 9)
+        offs = fuzz_text.random_cuts(rng, data, 6, anywhere=it % 5 == 4)
+        kw = {"index_bits": 64} if it % 3 == 1 else {}
+        h = _emu_vs_oracle(data, offs, **kw)
+        paths[h["path"]] += 1
+        if it % 4 != 3 and it % 10 != 9 and it % 5 != 4:
+            assert h["path"] == "fast", (it, data[:300])
+    assert paths["fast"] >= 20 and paths["exact"] >= 5, paths
+
+
 def test_emu_fast_equals_exact_synthetic():
     text, _ = synth.rows(synth.LIBSVM, 800, 40, seed=5)
     data = text.tobytes()

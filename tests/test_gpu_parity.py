@@ -262,6 +262,48 @@ def test_gpu_fast_dense_runs_vs_oracle(dm):
         assert h["path"] == "fast", (it, style)
 
 
+def test_gpu_fast_qid_vs_oracle(dm):
+    """"qid:" rows through the single-pass kernel (svm_fast.h qid_clean /
+    qid_ok, qid_fix_kernel): fast and exact paths both equal the oracle;
+    the reference's odd readings and rows without a qid take the exact path."""
+    rng = np.random.default_rng(8128)
+    paths = {"fast": 0, "exact": 0}
+    for it in range(120):
+        big = it % 10 == 0
+        data = fuzz_text.qid_libsvm(rng, 3000 if big else int(rng.integers(1, 40)), 60 if big else 16,
+                                    violate=it % 4 == 3, mixed=it % 10 == 9)
+        offs = fuzz_text.random_cuts(rng, data, int(rng.integers(0, 8)), anywhere=it % 5 == 4)
+        kw = {"index_bits": 64} if it % 3 == 1 else {}
+        h = _gpu_vs_oracle_paths(dm, data, offs, **kw)
+        paths[h["path"]] += 1
+        if it % 4 != 3 and it % 10 != 9 and it % 5 != 4:
+            assert h["path"] == "fast", it
+    assert paths["fast"] >= 60 and paths["exact"] >= 20, paths
+
+
+def test_gpu_qid_bench_size_fast_equals_exact(dm):
+    """The qid bench config (1M rows x 128 nnz, qid:<row/16> on every row):
+    single-pass == exact bit for bit, qid[r] = r / 16."""
+    import torch
+    text, _ = synth.rows(synth.LIBSVM_QID, 1 << 20, 128, seed=1)
+    starts = dm.text_chunk_starts(text)
+    d_text, d_cs = torch.from_numpy(text).cuda(), torch.from_numpy(starts).cuda()
+    outs = {}
+    for exact in (False, True):
+        p = dm.DeviceParser("libsvm", flags=dm.FLAG_EXACT if exact else 0)
+        out = p.parse(d_text, d_cs)
+        assert out["error"] == 0 and out["path"] == (1 if exact else 0)
+        outs[exact] = out
+    c = outs[False]["counts"]
+    assert c[:7] == outs[True]["counts"][:7] and c[dm.QID] == 1 << 20
+    for k in ("offset", "label", "qid", "index", "value"):
+        a, b = outs[False][k], outs[True][k]
+        assert torch.equal(a.view(torch.int32) if a.dtype == torch.float32 else a,
+                           b.view(torch.int32) if b.dtype == torch.float32 else b), k
+    q = outs[False]["qid"][: 1 << 20].to(torch.int64)
+    assert bool((q == torch.arange(1 << 20, device=q.device) // 16).all())
+
+
 def test_gpu_fast_synthetic_vs_oracle(dm):
     """~100 MB of canonical synthetic text (many tiles, 8 MiB InputSplit chunks)."""
     text, _ = synth.rows(synth.LIBSVM, 50000, 128, seed=21)
