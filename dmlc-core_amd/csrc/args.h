@@ -68,7 +68,8 @@ struct FastSvmArgs {
   float *value;
   uint64_t cap[8];
   uint64_t *chunk_tab;  // may be null
-  uint64_t *lb;         // look-back records [5 ntiles] (status words zeroed per launch), qid counts [ntiles]
+  uint64_t *lb;         // look-back records [5 ntiles] (status words zeroed per launch)
+  uint64_t *qsum;       // libsvm: qid runs, sharded by tile [kLabShards][8] (zeroed per launch)
   uint32_t *gate;       // != 0: input left the grammar -> exact path
   unsigned long long *err;  // first error of this path
   uint64_t *res;        // dmlc_amd_result counts (written by the last tile)

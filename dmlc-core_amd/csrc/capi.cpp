@@ -239,6 +239,7 @@ int dmlc_amd_parse(const void *d_text, uint64_t nbytes, const uint64_t *d_chunk_
     for (int i = 0; i < 8; ++i) f.cap[i] = out->cap[i];
     f.chunk_tab = d_chunk_table;
     f.lb = lb;
+    f.qsum = labsum;
     f.gate = ctl;
     f.err = ferr;
     f.res = res;

@@ -122,7 +122,7 @@ hipError_t launch_csv(const CsvArgs &a, const FastCsvArgs &f, bool use_fast, uin
     }
   }
   select_kernel<<<1, 1, 0, s>>>(res, gate, f.err);
-  if (phase != kPhaseCount && f.chunk_tab && f.nchunk > 0) chunk_fixup_kernel<<<1, 1, 0, s>>>(f.chunk_tab, f.nchunk, res);
+  if (phase != kPhaseCount && f.chunk_tab && f.nchunk > 0) chunk_fixup_kernel<<<1, 256, 0, s>>>(f.chunk_tab, f.nchunk, res);
   return hipGetLastError();
 }
 

@@ -111,7 +111,7 @@ hipError_t launch_libfm(const LibfmArgs &a, const FastSvmArgs &f, bool use_fast,
     }
   }
   fm_select_kernel<<<1, 1, 0, s>>>(res, gate, f.err);
-  if (phase != kPhaseCount && a.chunk_tab && a.nchunk > 0) chunk_fixup_kernel<<<1, 1, 0, s>>>(a.chunk_tab, a.nchunk, res);
+  if (phase != kPhaseCount && a.chunk_tab && a.nchunk > 0) chunk_fixup_kernel<<<1, 256, 0, s>>>(a.chunk_tab, a.nchunk, res);
   return hipGetLastError();
 }
 

@@ -50,19 +50,14 @@ __global__ void reopen_kernel(uint64_t *res, uint64_t *offset, uint64_t cap_rows
 // after the single-pass kernel: the tiles' qid run counts against the rows
 // (svm_fast.h qid_decide); when every row has a qid, each chunk row's qid
 // count is its row count
-__global__ void __launch_bounds__(256) qid_fix_kernel(const uint64_t *qcnt, uint32_t ntiles, uint64_t *res,
-                                                      uint32_t *gate, uint64_t *chunk_tab, int nchunk) {
-  __shared__ uint64_t part[256];
+__global__ void __launch_bounds__(256) qid_fix_kernel(const uint64_t *qsum, uint64_t *res, uint32_t *gate,
+                                                      uint64_t *chunk_tab, int nchunk) {
   __shared__ int fix_tab;
-  uint64_t sum = 0;
-  for (uint32_t i = threadIdx.x; i < ntiles; i += 256) sum += qcnt[i];
-  part[threadIdx.x] = sum;
-  __syncthreads();
-  for (int d = 128; d > 0; d >>= 1) {
-    if ((int)threadIdx.x < d) part[threadIdx.x] += part[threadIdx.x + d];
-    __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t total = 0;
+    for (int i = 0; i < kLabShards; ++i) total += qsum[i * 8];
+    fix_tab = fsvm::qid_decide(total, res, gate) && chunk_tab;
   }
-  if (threadIdx.x == 0) fix_tab = fsvm::qid_decide(part[0], res, gate) && chunk_tab;
   __syncthreads();
   if (fix_tab)
     for (int i = threadIdx.x; i < nchunk; i += 256) {
@@ -98,6 +93,7 @@ hipError_t launch_libsvm(const LibsvmArgs &a, const FastSvmArgs &f, bool use_fas
   if (use_fast) {
     if ((e = hipMemsetAsync(f.err, 0xFF, sizeof(uint64_t), s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(f.lb, 0, (size_t)f.ntiles * sizeof(uint64_t), s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(f.qsum, 0, kLabShards * 8 * sizeof(uint64_t), s)) != hipSuccess) return e;
     if (phase == kPhaseCount) {
       prof_mark(0, s, "svm_fast_tile<1>");
       svm_fast_tile<1><<<f.ntiles, kThreads, 0, s>>>(f);
@@ -107,8 +103,7 @@ hipError_t launch_libsvm(const LibsvmArgs &a, const FastSvmArgs &f, bool use_fas
       svm_fast_tile<2><<<f.ntiles, kThreads, 0, s>>>(f);
       prof_mark(1, s, "svm_fast_tile<2>");
     }
-    qid_fix_kernel<<<1, 256, 0, s>>>(f.lb + 5 * (uint64_t)f.ntiles, f.ntiles, res, gate,
-                                     phase != kPhaseCount ? f.chunk_tab : nullptr, f.nchunk);
+    qid_fix_kernel<<<1, 256, 0, s>>>(f.qsum, res, gate, phase != kPhaseCount ? f.chunk_tab : nullptr, f.nchunk);
   } else if ((e = hipMemsetAsync(f.err, 0xFF, sizeof(uint64_t), s)) != hipSuccess) {
     return e;
   }
@@ -147,7 +142,7 @@ hipError_t launch_libsvm(const LibsvmArgs &a, const FastSvmArgs &f, bool use_fas
     }
   }
   select_kernel<<<1, 1, 0, s>>>(res, gate, f.err);
-  if (phase != kPhaseCount && f.chunk_tab && f.nchunk > 0) chunk_fixup_kernel<<<1, 1, 0, s>>>(f.chunk_tab, f.nchunk, res);
+  if (phase != kPhaseCount && f.chunk_tab && f.nchunk > 0) chunk_fixup_kernel<<<1, 256, 0, s>>>(f.chunk_tab, f.nchunk, res);
   return hipGetLastError();
 }
 

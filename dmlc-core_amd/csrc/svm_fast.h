@@ -608,7 +608,7 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
   if (tid == 0) {
     publish_aggregate(a.lb, a.ntiles, k, cnt4);
     if (sh.c.bad) atomic_or_u32(a.gate, 1u);
-    if (!FM) a.lb[5 * (uint64_t)a.ntiles + k] = sh.nq;  // qid_fix_kernel's per-tile qid counts
+    if (!FM && sh.nq) atomic_add_u64(a.qsum + (k % kLabShards) * 8, sh.nq);  // qid_fix_kernel's sum
   }
   const uint64_t P = t.tlo + (uint64_t)tid * kSegB;
   const bool one_chunk = sh.c.ncs == 0;  // no chunk boundary before cnext

@@ -36,6 +36,9 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstdio>
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
@@ -303,12 +306,14 @@ struct EngineConfig {
   int per_device = 2;        // workers (HIP streams) per device
   int depth = 0;             // parsed batches ahead of the consumer (0: 2 per worker)
   bool max_index = false;    // reduce index/field maxima on the device (RowBlockIter::NumCol)
+  bool stats = false;        // DMLC_AMD_STATS=1: per-stage times on stderr when the parser ends
 
   // batch size, devices and workers from the environment
   // (DMLC_AMD_BATCH_BYTES, DMLC_AMD_DEVICES = "0,1,..." | "all", DMLC_AMD_WORKERS)
   void from_env() {
     batch_bytes = env_bytes("DMLC_AMD_BATCH_BYTES", batch_bytes, 1u << 20);
     if (const char *w = std::getenv("DMLC_AMD_WORKERS")) per_device = std::max(1, std::atoi(w));
+    if (const char *st = std::getenv("DMLC_AMD_STATS")) stats = std::atoi(st) != 0;
     if (const char *d = std::getenv("DMLC_AMD_DEVICES")) {
       devices.clear();
       int n = 0;
@@ -348,7 +353,10 @@ class HipTextParser : public dmlc::Parser<IndexType, DType> {
     for (int i = 0; i < nworkers; ++i) workers_.emplace_back(new Worker(cfg_.devices[i % cfg_.devices.size()]));
     Start();
   }
-  ~HipTextParser() override { Stop(); }
+  ~HipTextParser() override {
+    Stop();
+    if (cfg_.stats) PrintStats();
+  }
 
   void BeforeFirst() override {
     Stop();
@@ -397,11 +405,14 @@ class HipTextParser : public dmlc::Parser<IndexType, DType> {
     ~Worker() {
       if (stream) {
         (void)hipSetDevice(device);
+        for (auto &e : ev)
+          if (e) (void)hipEventDestroy(e);
         (void)hipStreamDestroy(stream);
       }
     }
     int device;
     hipStream_t stream = nullptr;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};  // stats: H2D | parse | D2H boundaries
     DevBuf text, cs, res, tab, ws, off, label, weight, qid, index, field, value;
     uint64_t cap[7] = {0, 0, 0, 0, 0, 0, 0};
     PinnedVec<dmlc_amd_result> hres;
@@ -439,6 +450,31 @@ class HipTextParser : public dmlc::Parser<IndexType, DType> {
     threads_.clear();
   }
 
+  // ---- pipeline statistics (DMLC_AMD_STATS): seconds summed over batches;
+  // the worker stages overlap each other and the reader, so the sums exceed
+  // the wall time.  Device stages are timed with HIP events on each stream.
+  enum { S_READ, S_H2D, S_PARSE, S_D2H, S_BUILD, S_WAIT, S_N };
+  std::atomic<uint64_t> stat_ns_[S_N] = {};
+  std::atomic<uint64_t> stat_batches_{0};
+  struct Clock {
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    uint64_t ns() const {
+      return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0)
+          .count();
+    }
+  };
+  void PrintStats() const {
+    static const char *kName[S_N] = {"read", "h2d", "parse", "d2h", "blocks", "consumer_wait"};
+    std::string line = "{\"dmlc_amd_stats\": {\"batches\": " + std::to_string(stat_batches_.load()) +
+                       ", \"workers\": " + std::to_string(workers_.size());
+    for (int i = 0; i < S_N; ++i) {
+      char buf[64];
+      std::snprintf(buf, sizeof(buf), ", \"%s_s\": %.4f", kName[i], stat_ns_[i].load() * 1e-9);
+      line += buf;
+    }
+    std::fprintf(stderr, "%s}}\n", line.c_str());
+  }
+
   void ReadLoop() {
     try {
       std::vector<uint64_t> ends;
@@ -452,6 +488,7 @@ class HipTextParser : public dmlc::Parser<IndexType, DType> {
           free_.pop_back();
         }
         b->clear_result();
+        const Clock clk;
         // room for one more whole chunk past the target (8 MiB InputSplit buffers)
         size_t cap = cfg_.batch_bytes + (16u << 20);
         b->text.reserve(cap);
@@ -468,6 +505,7 @@ class HipTextParser : public dmlc::Parser<IndexType, DType> {
         for (size_t i = 0; i < ends.size(); ++i) b->starts.p[i + 1] = ends[i];
         b->bytes = ends.empty() ? 0 : ends.back();
         b->end = f.end;
+        if (cfg_.stats) stat_ns_[S_READ] += clk.ns();
         {
           std::lock_guard<std::mutex> lk(mu_);
           b->seq = next_read_++;
@@ -516,8 +554,10 @@ class HipTextParser : public dmlc::Parser<IndexType, DType> {
   }
 
   B *Take() {
+    const Clock clk;
     std::unique_lock<std::mutex> lk(mu_);
     cv_.wait(lk, [&] { return done_.count(next_take_) || (!read_error_.empty() && next_take_ >= next_read_); });
+    if (cfg_.stats) stat_ns_[S_WAIT] += clk.ns();
     auto it = done_.find(next_take_);
     if (it == done_.end()) throw dmlc::Error(read_error_);
     B *b = it->second;
@@ -546,8 +586,13 @@ class HipTextParser : public dmlc::Parser<IndexType, DType> {
     uint64_t *d_res = static_cast<uint64_t *>(w->res.get(sizeof(dmlc_amd_result)));
     uint64_t *d_tab = static_cast<uint64_t *>(w->tab.get(nunits * 64));
     dmlc_amd_result *hres = w->hres.reserve(1);
+    const bool st = cfg_.stats;
+    if (st && !w->ev[0])
+      for (auto &e : w->ev) hip_check(hipEventCreate(&e), "hipEventCreate");
+    if (st) hip_check(hipEventRecord(w->ev[0], s), "hipEventRecord");
     hip_check(hipMemcpyAsync(d_text, b->text.p, b->bytes, hipMemcpyHostToDevice, s), "H2D text");
     hip_check(hipMemcpyAsync(d_cs, b->starts.p, (nch + 1) * 8, hipMemcpyHostToDevice, s), "H2D chunk starts");
+    if (st) hip_check(hipEventRecord(w->ev[1], s), "hipEventRecord");
     dmlc_amd_params p = cfg_.prm;
     p.flags = cfg_.max_index ? DMLC_AMD_FLAG_MAX_INDEX : 0u;
     const size_t ws = dmlc_amd_workspace_bytes(b->bytes, nch, &p);
@@ -561,6 +606,7 @@ class HipTextParser : public dmlc::Parser<IndexType, DType> {
       CheckRc(dmlc_amd_parse(d_text, b->bytes, d_cs, nch, &p, &out, d_tab, d_ws, ws,
                              reinterpret_cast<dmlc_amd_result *>(d_res), s));
       hip_check(hipMemcpyAsync(hres, d_res, sizeof(dmlc_amd_result), hipMemcpyDeviceToHost, s), "D2H result");
+      if (st) hip_check(hipEventRecord(w->ev[2], s), "hipEventRecord");
       hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
       if ((hres->error & 0xFFFF) != DMLC_AMD_ERR_CAPACITY) break;
       if (attempt > 0) throw dmlc::Error("dmlc_amd_parse: output capacity exceeded at exact sizes");
@@ -589,8 +635,19 @@ class HipTextParser : public dmlc::Parser<IndexType, DType> {
     d2h(b->field.reserve(c[DMLC_AMD_FIELD] + 1), out.field, c[DMLC_AMD_FIELD] * sizeof(IndexType));
     d2h(b->value.reserve(c[DMLC_AMD_VALUE] + 1), out.value, c[DMLC_AMD_VALUE] * sizeof(DType));
     d2h(b->tab.reserve(nunits * 8), d_tab, nunits * 64);
+    if (st) hip_check(hipEventRecord(w->ev[3], s), "hipEventRecord");
     hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
+    const Clock clk;
     BuildBlocks(b, nunits, upc);
+    if (st) {
+      float ms[3] = {0, 0, 0};
+      for (int i = 0; i < 3; ++i) hip_check(hipEventElapsedTime(&ms[i], w->ev[i], w->ev[i + 1]), "hipEventElapsedTime");
+      stat_ns_[S_H2D] += (uint64_t)(ms[0] * 1e6);
+      stat_ns_[S_PARSE] += (uint64_t)(ms[1] * 1e6);
+      stat_ns_[S_D2H] += (uint64_t)(ms[2] * 1e6);
+      stat_ns_[S_BUILD] += clk.ns();
+      ++stat_batches_;
+    }
   }
 
   void Outputs(Worker *w, const uint64_t *want, dmlc_amd_csr *out) {

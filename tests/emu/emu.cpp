@@ -197,7 +197,7 @@ extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *c
     const uint64_t nft = (nbytes + fsvm::kTile - 1) / fsvm::kTile;
     uint32_t gate = use_fast ? 0u : 1u;
     unsigned long long ferr = ~0ull;
-    std::vector<uint64_t> lb(nft * 8 + 1, 0);
+    std::vector<uint64_t> lb(nft * 8 + 1, 0), qsum(kLabShards * 8, 0);
     LibfmArgs a;
     std::memset(&a, 0, sizeof(a));
     a.field = out->field;
@@ -243,6 +243,7 @@ extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *c
       for (int i = 0; i < 8; ++i) f.cap[i] = out->cap[i];
       f.chunk_tab = chunk_table;
       f.lb = lb.data();
+      f.qsum = qsum.data();
       f.gate = &gate;
       f.err = &ferr;
       f.res = res;
@@ -262,7 +263,7 @@ extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *c
       }
       if (!fm) {  // qid_fix_kernel (libsvm.hip)
         uint64_t total = 0;
-        for (uint64_t k = 0; k < nft; ++k) total += lb[5 * nft + k];
+        for (int i = 0; i < kLabShards; ++i) total += qsum[i * 8];
         if (fsvm::qid_decide(total, res, &gate) && chunk_table && !count_only)
           for (int i = 0; i < nchunks; ++i)
             if (chunk_table[i * 8 + C_ROWS] != ~0ull) chunk_table[i * 8 + C_QID] = chunk_table[i * 8 + C_ROWS];
