@@ -221,6 +221,43 @@ class InputSplitSource : public ChunkSource {
 
 // -------------------------------------------------------------- buffers --
 
+// Process-wide cache of page-locked blocks: pinning is slow (hipHostMalloc
+// maps and locks every page), and each parser holds a batch pool of several
+// hundred MB, so parsers created one after another (a Parser per file or per
+// epoch) reuse the blocks instead of pinning them again.  Blocks are kept for
+// the life of the process.
+class PinnedCache {
+ public:
+  static PinnedCache &get() {
+    static PinnedCache *c = new PinnedCache();  // never destroyed: no HIP call at process exit
+    return *c;
+  }
+  void *take(size_t bytes, size_t *got) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      auto it = free_.lower_bound(bytes);
+      if (it != free_.end() && it->first <= 2 * bytes) {
+        void *p = it->second;
+        *got = it->first;
+        free_.erase(it);
+        return p;
+      }
+    }
+    void *p = nullptr;
+    hip_check(hipHostMalloc(&p, bytes, hipHostMallocPortable), "hipHostMalloc");
+    *got = bytes;
+    return p;
+  }
+  void give(void *p, size_t bytes) {
+    std::lock_guard<std::mutex> lk(mu_);
+    free_.emplace(bytes, p);
+  }
+
+ private:
+  std::mutex mu_;
+  std::multimap<size_t, void *> free_;
+};
+
 template <typename T>
 struct PinnedVec {  // page-locked host array, grown on demand (contents not kept)
   T *p = nullptr;
@@ -229,15 +266,14 @@ struct PinnedVec {  // page-locked host array, grown on demand (contents not kep
   PinnedVec(const PinnedVec &) = delete;
   PinnedVec &operator=(const PinnedVec &) = delete;
   ~PinnedVec() {
-    if (p) (void)hipHostFree(p);
+    if (p) PinnedCache::get().give(p, cap * sizeof(T));
   }
   T *reserve(size_t n) {
     if (n > cap) {
-      if (p) hip_check(hipHostFree(p), "hipHostFree");
-      p = nullptr;
-      const size_t c = n + n / 4 + 64;
-      hip_check(hipHostMalloc(reinterpret_cast<void **>(&p), c * sizeof(T), hipHostMallocPortable), "hipHostMalloc");
-      cap = c;
+      if (p) PinnedCache::get().give(p, cap * sizeof(T));
+      size_t got = 0;
+      p = static_cast<T *>(PinnedCache::get().take((n + n / 4 + 64) * sizeof(T), &got));
+      cap = got / sizeof(T);
     }
     return p;
   }

@@ -205,7 +205,7 @@ void TextSplit::ReadAt(char *buf, size_t len, uint64_t pos) {
   static const size_t kThreadsMax = [] {
     const char *e = std::getenv("DMLC_AMD_READ_THREADS");
     const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-    return (size_t)std::min<unsigned>(e ? std::max(1, std::atoi(e)) : 4u, hw);
+    return (size_t)std::min<unsigned>(e ? std::max(1, std::atoi(e)) : 8u, hw);
   }();
   const size_t nt = std::min<size_t>(kThreadsMax, len / kMinSplit);
   if (nt <= 1) {

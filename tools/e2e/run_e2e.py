@@ -38,8 +38,8 @@ def main():
         line["config"] = name
         # one more pass with the engine's per-stage times (DMLC_AMD_STATS): seconds summed over
         # batches; the reader, the workers' H2D / parse / D2H and the consumer overlap
-        r2 = subprocess.run([exe, path, fmt, "1"], capture_output=True, text=True, timeout=600,
-                            env=dict(os.environ, DMLC_AMD_STATS="1"))
+        r2 = subprocess.run([exe, path, fmt, "3"], capture_output=True, text=True, timeout=600,
+                            env=dict(os.environ, DMLC_AMD_STATS="1"))  # stats of the last (warm) pass
         st = [json.loads(x) for x in r2.stderr.splitlines() if x.startswith('{"dmlc_amd_stats"')]
         line["stages"] = st[-1]["dmlc_amd_stats"] if st else None
         line["stages_pass_s"] = json.loads(r2.stdout)["best_s"] if r2.returncode == 0 else None
