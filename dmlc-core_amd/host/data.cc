@@ -202,14 +202,166 @@ class HipRowIter : public dmlc::RowBlockIter<I, D> {
   dmlc::RowBlock<I, D> row_;
 };
 
+// ---- the #cache path: RowBlockContainer pages on disk (disk_row_iter.h)
+
+// A page: the reference's RowBlockContainer (row_block.h:27-216) -- Push of
+// RowBlocks with offset rebasing and index / field maxima, MemCostBytes,
+// and the Save / Load byte format (each vector as u64 count + raw elements,
+// then max_field and max_index as IndexType).
+template <typename I, typename D>
+struct Page {
+  std::vector<size_t> offset{0};
+  std::vector<D> label, value;
+  std::vector<float> weight;
+  std::vector<uint64_t> qid;
+  std::vector<I> field, index;
+  I max_field = 0, max_index = 0;
+
+  void Clear() {
+    offset.assign(1, 0);
+    label.clear();
+    value.clear();
+    weight.clear();
+    qid.clear();
+    field.clear();
+    index.clear();
+    max_field = max_index = 0;
+  }
+  size_t Size() const { return offset.size() - 1; }
+  size_t MemCostBytes() const {  // row_block.h:81-86 (labels and weights priced as real_t)
+    return offset.size() * sizeof(size_t) + label.size() * sizeof(dmlc::real_t) +
+           weight.size() * sizeof(dmlc::real_t) + qid.size() * sizeof(size_t) + field.size() * sizeof(I) +
+           index.size() * sizeof(I) + value.size() * sizeof(D);
+  }
+  // row_block.h:126-168; a block without labels (label-less CSV) pushes zeros
+  // where the reference copies from its NULL label pointer
+  void Push(const dmlc::RowBlock<I, D> &b) {
+    const size_t n0 = label.size();
+    label.resize(n0 + b.size);
+    if (b.label) std::memcpy(label.data() + n0, b.label, b.size * sizeof(D));
+    if (b.weight) weight.insert(weight.end(), b.weight, b.weight + b.size);
+    if (b.qid) qid.insert(qid.end(), b.qid, b.qid + b.size);
+    const size_t ndata = b.offset[b.size] - b.offset[0];
+    if (b.field) {
+      field.insert(field.end(), b.field, b.field + ndata);
+      for (size_t i = 0; i < ndata; ++i) max_field = std::max(max_field, b.field[i]);
+    }
+    index.insert(index.end(), b.index, b.index + ndata);
+    for (size_t i = 0; i < ndata; ++i) max_index = std::max(max_index, b.index[i]);
+    if (b.value) value.insert(value.end(), b.value, b.value + ndata);
+    const size_t shift = offset.back();
+    for (size_t i = 0; i < b.size; ++i) offset.push_back(shift + b.offset[i + 1] - b.offset[0]);
+  }
+  void Save(dmlc::Stream *fo) const {
+    fo->Write(offset);
+    fo->Write(label);
+    fo->Write(weight);
+    fo->Write(qid);
+    fo->Write(field);
+    fo->Write(index);
+    fo->Write(value);
+    fo->Write(&max_field, sizeof(I));
+    fo->Write(&max_index, sizeof(I));
+  }
+  bool Load(dmlc::Stream *fi) {
+    if (!fi->Read(&offset)) return false;
+    CHECK(fi->Read(&label)) << "Bad RowBlock format";
+    CHECK(fi->Read(&weight)) << "Bad RowBlock format";
+    CHECK(fi->Read(&qid)) << "Bad RowBlock format";
+    CHECK(fi->Read(&field)) << "Bad RowBlock format";
+    CHECK(fi->Read(&index)) << "Bad RowBlock format";
+    CHECK(fi->Read(&value)) << "Bad RowBlock format";
+    CHECK(fi->Read(&max_field, sizeof(I)) == sizeof(I)) << "Bad RowBlock format";
+    CHECK(fi->Read(&max_index, sizeof(I)) == sizeof(I)) << "Bad RowBlock format";
+    return true;
+  }
+  // GetBlock (row_block.h:171-189) with its CHECKs
+  dmlc::RowBlock<I, D> Block() const {
+    CHECK(label.size() + 1 == offset.size());
+    CHECK(offset.back() == index.size());
+    CHECK(offset.back() == value.size() || value.size() == 0);
+    dmlc::RowBlock<I, D> b;
+    b.size = Size();
+    b.offset = offset.data();
+    b.label = dmlc::BeginPtr(label);
+    b.weight = dmlc::BeginPtr(weight);
+    b.qid = dmlc::BeginPtr(qid);
+    b.field = dmlc::BeginPtr(field);
+    b.index = dmlc::BeginPtr(index);
+    b.value = dmlc::BeginPtr(value);
+    return b;
+  }
+};
+
+// DiskRowIter (disk_row_iter.h:40-137): with `uri#cachefile` the parsed rows
+// are written once to the cache file in 64 MB pages (RowBlockContainer::Save)
+// and the iterator reads the pages back; an existing cache file is reused
+// without parsing.  NumCol: max_index + 1 over the pages built (as the
+// reference); when an existing cache is reused the reference leaves it
+// uninitialised -- here the pages are scanned once for it.
+template <typename I, typename D>
+class HipDiskRowIter : public dmlc::RowBlockIter<I, D> {
+ public:
+  static const size_t kPageSize = 64UL << 20UL;  // disk_row_iter.h:34
+  HipDiskRowIter(dmlc::Parser<I, D> *parser, const std::string &cache_file) : cache_file_(cache_file) {
+    std::unique_ptr<dmlc::Parser<I, D>> p(parser);
+    if (!TryLoadCache()) {
+      BuildCache(p.get());
+      CHECK(TryLoadCache()) << "failed to build cache file " << cache_file_;
+    } else {
+      ScanNumCol();
+    }
+  }
+  void BeforeFirst() override { fi_->Seek(0); }
+  bool Next() override {
+    if (!page_.Load(fi_.get())) return false;
+    row_ = page_.Block();
+    return true;
+  }
+  const dmlc::RowBlock<I, D> &Value() const override { return row_; }
+  size_t NumCol() const override { return num_col_; }
+
+ private:
+  bool TryLoadCache() {
+    fi_.reset(dmlc::SeekStream::CreateForRead(cache_file_.c_str(), true));
+    return fi_ != nullptr;
+  }
+  void BuildCache(dmlc::Parser<I, D> *parser) {
+    std::unique_ptr<dmlc::Stream> fo(dmlc::Stream::Create(cache_file_.c_str(), "w"));
+    Page<I, D> data;
+    num_col_ = 0;
+    while (parser->Next()) {
+      data.Push(parser->Value());
+      if (data.MemCostBytes() >= kPageSize) {
+        num_col_ = std::max(num_col_, static_cast<size_t>(data.max_index) + 1);
+        data.Save(fo.get());
+        data.Clear();
+      }
+    }
+    if (data.Size() != 0) {
+      num_col_ = std::max(num_col_, static_cast<size_t>(data.max_index) + 1);
+      data.Save(fo.get());
+    }
+  }
+  void ScanNumCol() {
+    num_col_ = 0;
+    while (page_.Load(fi_.get())) num_col_ = std::max(num_col_, static_cast<size_t>(page_.max_index) + 1);
+    fi_->Seek(0);
+  }
+
+  std::string cache_file_;
+  std::unique_ptr<dmlc::SeekStream> fi_;
+  size_t num_col_ = 0;
+  Page<I, D> page_;
+  dmlc::RowBlock<I, D> row_;
+};
+
 template <typename I, typename D>
 dmlc::RowBlockIter<I, D> *CreateIter_(const char *uri, unsigned part, unsigned nparts, const char *type) {
   UriSpec spec(uri, part, nparts);
-  if (!spec.cache_file.empty())
-    LOG(WARNING) << "#" << spec.cache_file << ": the disk row cache is out of this build's scope; parsing in memory";
   // as the reference (data.cc:88-105): the parser is created from spec.uri,
   // i.e. WITHOUT the ?key=value arguments of the RowBlockIter uri
-  g_want_max_index = true;  // NumCol from the device maxima (this build's parsers)
+  g_want_max_index = spec.cache_file.empty();  // NumCol from the device maxima (this build's parsers)
   dmlc::Parser<I, D> *parser;
   try {
     parser = CreateParser_<I, D>(spec.uri.c_str(), part, nparts, type);
@@ -218,6 +370,7 @@ dmlc::RowBlockIter<I, D> *CreateIter_(const char *uri, unsigned part, unsigned n
     throw;
   }
   g_want_max_index = false;
+  if (!spec.cache_file.empty()) return new HipDiskRowIter<I, D>(parser, spec.cache_file);
   return new HipRowIter<I, D>(parser);
 }
 

@@ -141,3 +141,28 @@ def test_plugin_args_auto_and_errors(tmp_path):
     assert "sign == true" in ref["error"] and "sign == true" in hip["error"]
     bad = run(tmp_path, d + "?bogus=1", "csv_hip", tag="h")
     assert "Cannot find argument" in bad["error"]
+
+
+@pytest.mark.gpu
+def test_disk_row_cache_pages_vs_reference(tmp_path):
+    """uri#cachefile (DiskRowIter, disk_row_iter.h:40-137): the rows written
+    once to 64 MB pages in RowBlockContainer::Save's format and read back.
+    The reference's own "libsvm" type, the HIP parser as a plugin of the
+    reference ("libsvm_hip"), and this build's drop-in API all write the same
+    cache file byte for byte and iterate the same pages; an existing cache is
+    reused without parsing."""
+    from test_host_api import run_api
+    text, _ = synth.rows(synth.LIBSVM, 100000, 128, seed=17)
+    d = write(tmp_path / "cache_in", {"f0": text.tobytes()})
+    caches = {k: str(tmp_path / ("%s.cache" % k)) for k in ("ref", "plugin", "dropin")}
+    ref = run(tmp_path, d + "#" + caches["ref"], "libsvm", iter_=True, tag="r")
+    plug = run(tmp_path, d + "#" + caches["plugin"], "libsvm_hip", iter_=True, tag="p")
+    drop = run_api(tmp_path, d + "#" + caches["dropin"], iter_=True)
+    raw = {k: open(v, "rb").read() for k, v in caches.items()}
+    assert len(raw["ref"]) > 64 << 20 and raw["plugin"] == raw["ref"] and raw["dropin"] == raw["ref"]
+    assert len(ref["blocks"]) >= 2  # pages
+    assert same(ref, plug) and same(ref, drop)
+    assert ref["meta"][2] == plug["meta"][2] == drop["meta"][2] > 0  # NumCol of a built cache
+    again = run_api(tmp_path, d + "#" + caches["dropin"], iter_=True)  # reuse: no parse
+    assert same(again, drop) and again["meta"][2] == drop["meta"][2]
+    assert open(caches["dropin"], "rb").read() == raw["ref"]
