@@ -389,9 +389,70 @@ DA_HD uint32_t fm_role_of(const Tile &t, uint64_t q, uint64_t f) {
 }
 
 struct SegOutFm {
-  uint64_t L, W, I, V, F;
+  uint64_t L, W, I, V, F, RS;
+  uint64_t q0;  // start of the last run that starts before the segment (kNone: none in its chunk)
   uint32_t bad;
 };
+
+// libfm carry-in from the 64 bytes before a segment (bit i <-> P-64+i), as
+// carry_fast does for libsvm, when no chunk starts in them and the last run
+// before P, its gap and the runs its role depends on lie inside them: the
+// role follows the ':'-chain back to its label or field (fm_role_of) over at
+// most three gaps.  *qlast: the window bit where that run starts.
+// kind of the gap in front of the run at bit q: 0 newline, 1 ':', 2 plain;
+// -1 when it or the run before it leaves the window (*qprev: that run's start)
+DA_HD int fm_gap(uint64_t d1, uint64_t n1, uint64_t c1, uint32_t q, uint32_t *qprev) {
+  const uint64_t below = d1 & ((1ull << q) - 1);
+  if (!below) return -1;
+  const uint32_t p = 63 - clz64(below);  // last byte of the run before
+  const uint64_t gm = ((1ull << q) - 1) & ~((2ull << p) - 1);
+  if (n1 & gm) return 0;
+  const uint64_t nd = ~d1 & ((1ull << p) - 1);
+  if (!nd) return -1;
+  *qprev = 64 - clz64(nd);
+  return (c1 & gm) ? 1 : 2;
+}
+DA_HD bool carry_fast_fm(uint64_t d1, uint64_t n1, uint64_t c1, uint32_t *dc, uint32_t *ginl, uint32_t *ginc,
+                         uint32_t *prole, uint32_t *qlast) {
+  *dc = (uint32_t)(d1 >> 63);
+  uint32_t qb;
+  if (*dc) {
+    const uint64_t nd = ~d1;
+    if (!nd) return false;
+    qb = 64 - clz64(nd);
+    *ginl = *ginc = 0;
+  } else {
+    if (!d1) return false;
+    const uint32_t pb = 63 - clz64(d1);
+    const uint64_t tg = ~0ull << (pb + 1);
+    const uint64_t tgn = n1 & tg;
+    *ginl = tgn != 0;
+    const uint32_t ln = tgn ? 63 - clz64(tgn) : 0;
+    const uint64_t after = !tgn ? tg : (ln == 63 ? 0ull : ~0ull << (ln + 1));
+    *ginc = (c1 & after) != 0;
+    const uint64_t nd = ~d1 & ((1ull << pb) - 1);
+    if (!nd) return false;
+    qb = 64 - clz64(nd);
+  }
+  *qlast = qb;
+  uint32_t q2 = 0, q3 = 0, q4 = 0;
+  const int g1 = fm_gap(d1, n1, c1, qb, &q2);
+  if (g1 < 0) return false;
+  if (g1 != 1) {
+    *prole = g1 == 0 ? RF_L : RF_F;
+    return true;
+  }
+  const int g2 = fm_gap(d1, n1, c1, q2, &q3);  // a ':' run: after a label W, after a field I
+  if (g2 < 0) return false;
+  if (g2 != 1) {
+    *prole = g2 == 0 ? RF_W : RF_I;
+    return true;
+  }
+  const int g3 = fm_gap(d1, n1, c1, q3, &q4);  // two ':' gaps: V after an index, else re-paired
+  if (g3 < 0) return false;
+  *prole = g3 == 2 ? RF_V : RF_BAD;
+  return true;
+}
 
 // previous-run propagation: bit x of the result = the run before run start x
 // has its start bit in X (cin: the run before the segment does)
@@ -402,7 +463,8 @@ DA_HD uint64_t prev_of(uint64_t RS, uint64_t X, uint32_t cin) {
 
 DA_HD SegOutFm segment_roles_fm(const Tile &t, int tid) {
   SegOutFm o;
-  o.L = o.W = o.I = o.V = o.F = 0;
+  o.L = o.W = o.I = o.V = o.F = o.RS = 0;
+  o.q0 = kNone;
   o.bad = 0;
   const FastSvmArgs &a = *t.a;
   const uint64_t P = t.tlo + (uint64_t)tid * kSegB;
@@ -415,16 +477,23 @@ DA_HD SegOutFm segment_roles_fm(const Tile &t, int tid) {
     const uint64_t x = t.sh->c.csl[i];
     if (x >= P && x < P + (uint64_t)nv) S |= 1ull << (x - P);
   }
-  // ---- carry-in (the general look-back over the LDS masks)
-  uint32_t dc = 0, ginl = 0, ginc = 0, prole = RF_NONE;
+  // ---- carry-in: from the previous segment's masks, else the general
+  // look-back over the LDS masks
+  uint32_t dc = 0, ginl = 0, ginc = 0, prole = RF_NONE, qb = 0;
   const uint64_t F = t.floor_of(P);
-  if (P != F) {
+  if (P != F && F + 64 <= P &&
+      carry_fast_fm(t.sh->u.m.d[tid], t.sh->u.m.n[tid], t.sh->u.m.c[tid], &dc, &ginl, &ginc, &prole, &qb)) {
+    o.q0 = P - 64 + qb;
+  } else if (P != F) {
+    dc = ginl = ginc = 0;
+    prole = RF_NONE;
     uint64_t d, n, c;
     t.seg((P - 1) >> 6, &d, &n, &c);
     dc = (uint32_t)(d >> 63) & 1u;
     if (dc) {
       const uint64_t x = t.last_bit(1, F, P);
-      prole = fm_role_of(t, x == kNone ? F : x + 1, F);
+      o.q0 = x == kNone ? F : x + 1;
+      prole = fm_role_of(t, o.q0, F);
     } else {
       const uint64_t p = t.last_bit(0, F, P);
       if (p == kNone) {
@@ -434,7 +503,8 @@ DA_HD SegOutFm segment_roles_fm(const Tile &t, int tid) {
         ginl = ln != kNone;
         ginc = t.last_bit(3, ginl ? ln + 1 : p + 1, P) != kNone;
         const uint64_t x = t.last_bit(1, F, p);
-        prole = fm_role_of(t, x == kNone ? F : x + 1, F);
+        o.q0 = x == kNone ? F : x + 1;
+        prole = fm_role_of(t, o.q0, F);
       }
     }
   }
@@ -456,11 +526,15 @@ DA_HD SegOutFm segment_roles_fm(const Tile &t, int tid) {
   const uint64_t I = K & prev_of(RS, Fr, prole == RF_F);
   const uint64_t V = K & prev_of(RS, I, prole == RF_I);
   if (K & ~(W | I | V)) o.bad = 1;
+  // an index's field is the run before it; the first one's may start before
+  // the segment (q0) -- further back than the staged pre-halo leaves the path
+  if ((I & RS & (0 - RS)) && (o.q0 == kNone || o.q0 + kPre < t.tlo)) o.bad = 1;
   o.L = L;
   o.W = W;
   o.I = I;
   o.V = V;
   o.F = Fr;
+  o.RS = RS;
   return o;
 }
 
@@ -577,7 +651,8 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
 #endif
   // ---- roles, counts, eligibility
   SegOut so;
-  uint64_t soF = 0;  // libfm: every field run (v1), for the sign check
+  so.Q = 0;
+  uint64_t soF = 0, soRS = 0, soQ0 = kNone;  // libfm: field runs (v1), all run starts, the run before
   if constexpr (FM) {
     const SegOutFm sf = segment_roles_fm(t, tid);
     so.L = sf.L;
@@ -586,6 +661,8 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
     so.V = sf.V;
     so.bad = sf.bad;
     soF = sf.F;
+    soRS = sf.RS;
+    soQ0 = sf.q0;
   } else {
     so = segment_roles(t, tid);
     if (so.Q) atomic_add_u32(&sh.nq, (uint32_t)popc64(so.Q));
@@ -692,67 +769,58 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
   // runs than fit is done in passes of consecutive segments.
   uint32_t np = 1, mypass = 0;
   uint64_t pe0 = totp;  // packed inclusive counts at the end of pass 0
+  // libfm adds a field list after the indices: entry j = the staged offset
+  // (tile offset + kPre) of index j's field run, the run before it
   auto build = [&](uint64_t s, uint64_t e) {  // my runs into the lists of the pass [s, e)
     const uint64_t rel = ex - s, cn = e - s;
     const uint32_t nIp = fI(cn), nVp = fV(cn), nLp = fL(cn);
     const uint32_t o0 = (uint32_t)tid * kSegB;
     uint32_t x = fI(rel);
     for (uint64_t m = so.I; m; m &= m - 1) sh.u.lst[x++] = (uint16_t)(o0 + ctz64(m));
-    x = nIp + fV(rel);
+    uint32_t fb0 = nIp;  // first float entry
+    if constexpr (FM) {
+      x = nIp + fI(rel);
+      for (uint64_t m = so.I; m; m &= m - 1) {
+        const uint64_t before = soRS & ((m & (0 - m)) - 1);
+        const uint64_t fpos = before ? P + 63 - clz64(before) : soQ0;  // checked >= tlo - kPre (roles)
+        sh.u.lst[x++] = (uint16_t)(fpos + kPre - t.tlo);
+      }
+      fb0 = 2 * nIp;
+    }
+    x = fb0 + fV(rel);
     for (uint64_t m = so.V; m; m &= m - 1) sh.u.lst[x++] = (uint16_t)(o0 + ctz64(m));
-    x = nIp + nVp + fL(rel);
+    x = fb0 + nVp + fL(rel);
     for (uint64_t m = so.L; m; m &= m - 1) sh.u.lst[x++] = (uint16_t)(o0 + ctz64(m));
-    x = nIp + nVp + nLp + fW(rel);
+    x = fb0 + nVp + nLp + fW(rel);
     for (uint64_t m = so.W; m; m &= m - 1) sh.u.lst[x++] = (uint16_t)(o0 + ctz64(m));
   };
-  uint32_t fpos = 0;  // libfm: bit positions of the batch's float runs, 6 bits each
-  uint64_t mI = so.I, mF = so.V | so.L | so.W;
   if (MODE == 2) {
-    if constexpr (!FM) {
-      // (the block scan's barriers ordered every plane read before these writes)
-      if (nL + nW + nI + nV > kPassRuns) {  // block-uniform: several passes
-        const uint32_t own = fL(mine) + fW(mine) + fI(mine) + fV(mine);
-        const uint32_t tex = fL(ex) + fW(ex) + fI(ex) + fV(ex);
-        mypass = tex / kPassRuns;
-        if (tid == kThreads - 1 || (tex + own) / kPassRuns != mypass) sh.pend[mypass] = ex + mine;
-        if (tid == kThreads - 1) sh.npass = mypass + 1;
-        bk.sync();
-        np = sh.npass;
-        pe0 = sh.pend[0];
-      }
-      if (mypass == 0) build(0, pe0);
+    // (the block scan's barriers ordered every plane read before these writes)
+    constexpr uint32_t kIW = FM ? 2u : 1u;  // list entries per index (libfm: + its field)
+    if (nL + nW + kIW * nI + nV > kPassRuns) {  // block-uniform: several passes
+      const uint32_t own = fL(mine) + fW(mine) + kIW * fI(mine) + fV(mine);
+      const uint32_t tex = fL(ex) + fW(ex) + kIW * fI(ex) + fV(ex);
+      mypass = tex / kPassRuns;
+      if (tid == kThreads - 1 || (tex + own) / kPassRuns != mypass) sh.pend[mypass] = ex + mine;
+      if (tid == kThreads - 1) sh.npass = mypass + 1;
       bk.sync();
-      FAST_STAMP(k, 5);
-      // ---- first decode batch into registers (gives predecessors time to publish)
-      const uint32_t nI0 = fI(pe0), nF0 = fV(pe0) + fL(pe0) + fW(pe0);
-#pragma unroll
-      for (int u = 0; u < kB; ++u) {
-        const uint32_t j = (uint32_t)tid + (uint32_t)u * kThreads;
-        ib[u] = 0;
-        fb[u] = 0.f;
-        if (j < nI0) ib[u] = dec_index(sh.u.lst[j]);
-        if (j < nF0) fb[u] = dec_float(sh.u.lst[nI0 + j]);
-      }
-      FAST_STAMP(k, 6);
-    } else {
-      // libfm: each thread decodes its own segment's runs (values, labels and
-      // weights in one position-ordered float stream)
-#pragma unroll
-      for (int u = 0; u < kB; ++u) {
-        ib[u] = 0;
-        fb[u] = 0.f;
-        if (mI) {
-          ib[u] = dec_index((uint32_t)(P - t.tlo) + ctz64(mI));
-          mI &= mI - 1;
-        }
-        if (mF) {
-          const uint32_t bpos = (uint32_t)ctz64(mF);
-          fb[u] = dec_float((uint32_t)(P - t.tlo) + bpos);
-          fpos |= bpos << (6 * u);
-          mF &= mF - 1;
-        }
-      }
+      np = sh.npass;
+      pe0 = sh.pend[0];
     }
+    if (mypass == 0) build(0, pe0);
+    bk.sync();
+    FAST_STAMP(k, 5);
+    // ---- first decode batch into registers (gives predecessors time to publish)
+    const uint32_t nI0 = fI(pe0), nF0 = fV(pe0) + fL(pe0) + fW(pe0), fb0 = kIW * nI0;
+#pragma unroll
+    for (int u = 0; u < kB; ++u) {
+      const uint32_t j = (uint32_t)tid + (uint32_t)u * kThreads;
+      ib[u] = 0;
+      fb[u] = 0.f;
+      if (j < nI0) ib[u] = dec_index(sh.u.lst[j]);
+      if (j < nF0) fb[u] = dec_float(sh.u.lst[fb0 + j]);
+    }
+    FAST_STAMP(k, 6);
   }
   // ---- decoupled look-back by wave 0 (fast_common.h)
 #ifdef FSVM_ABL_NOLB  // timing ablation only: write pass without look-back (bases k * counts, in bounds)
@@ -828,124 +896,90 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
     if (r < a.cap[C_WEIGHT]) a.weight[r] = v;
     else raise_error(a.err, E_CAPACITY, q);
   };
-  if constexpr (!FM) {
-    // entry j of the float list of the pass starting at packed counts s
-    auto put_float = [&](uint32_t j, float v, uint32_t o, uint64_t s, uint32_t nVp, uint32_t nLp) {
-      const uint64_t q = t.tlo + o;
-      if (j < nVp) put_value(bVal + fV(s) + j, v, q);
-      else if (j < nVp + nLp) put_label(bRows + fL(s) + (j - nVp), v, q);
-      else put_weight(bW + fW(s) + (j - nVp - nLp), v, q);
-    };
-    {  // the register batch (pass 0)
-      const uint32_t nI0 = fI(pe0), nV0 = fV(pe0), nL0 = fL(pe0), nF0 = nV0 + nL0 + fW(pe0);
+  // entry j of the float list of the pass starting at packed counts s
+  auto put_float = [&](uint32_t j, float v, uint32_t o, uint64_t s, uint32_t nVp, uint32_t nLp) {
+    const uint64_t q = t.tlo + o;
+    if (j < nVp) put_value(bVal + fV(s) + j, v, q);
+    else if (j < nVp + nLp) put_label(bRows + fL(s) + (j - nVp), v, q);
+    else put_weight(bW + fW(s) + (j - nVp - nLp), v, q);
+  };
+  // libfm: the field run at staged offset so (a window when it lies inside
+  // its chunk; a '-' is raised by the sign check below)
+  auto put_field = [&](uint64_t r, uint32_t so) {
+    const uint64_t q = t.tlo + so - kPre;
+    const uint64_t lim = lim_of(q);
+    uint64_t v = 0;
+    bool ok = false, pos = true;
+    if (q + 16 <= lim) {
+      const W16 wq = win_at(sh.c.text, t.tlo, q);
+      const uint32_t w4[4] = {(uint32_t)wq.lo, (uint32_t)(wq.lo >> 32), (uint32_t)wq.hi, (uint32_t)(wq.hi >> 32)};
+      pos = wuint32(w4, sh.dt, &v, &ok);
+    }
+    if (!ok) pos = slow_uint(a.text, q, lim, a.wide, &v);
+    if (!pos) v = 0;
+    if (a.indexing_mode > 0) --v;
+    if (r < a.cap[C_FIELD]) {
+      if (a.wide) reinterpret_cast<uint64_t *>(a.field)[r] = v;
+      else reinterpret_cast<uint32_t *>(a.field)[r] = (uint32_t)v;
+    } else {
+      raise_error(a.err, E_CAPACITY, q);
+    }
+  };
+  constexpr uint32_t kIW = FM ? 2u : 1u;  // list entries per index
+  {  // the register batch (pass 0)
+    const uint32_t nI0 = fI(pe0), nV0 = fV(pe0), nL0 = fL(pe0), nF0 = nV0 + nL0 + fW(pe0), fb0 = kIW * nI0;
 #pragma unroll
-      for (int u = 0; u < kB; ++u) {
-        const uint32_t j = (uint32_t)tid + (uint32_t)u * kThreads;
-        if (j < nI0) put_index(bIdx + j, ib[u], t.tlo + sh.u.lst[j]);
-        if (j < nF0) put_float(j, fb[u], sh.u.lst[nI0 + j], 0, nV0, nL0);
-      }
+    for (int u = 0; u < kB; ++u) {
+      const uint32_t j = (uint32_t)tid + (uint32_t)u * kThreads;
+      if (j < nI0) put_index(bIdx + j, ib[u], t.tlo + sh.u.lst[j]);
+      if (j < nF0) put_float(j, fb[u], sh.u.lst[fb0 + j], 0, nV0, nL0);
     }
-    for (uint32_t p = 0; p < np; ++p) {
-      const uint64_t s = p ? sh.pend[p - 1] : 0, e = p ? sh.pend[p] : pe0;
-      if (p) {  // block-uniform
-        bk.sync();
-        if (mypass == p) build(s, e);
-        bk.sync();
-      }
-      const uint64_t cn = e - s;
-      const uint32_t nIp = fI(cn), nVp = fV(cn), nLp = fL(cn), nFp = nVp + nLp + fW(cn);
-      const uint32_t j0 = (uint32_t)tid + (p ? 0u : (uint32_t)kB * kThreads);
-      for (uint32_t j = j0; j < nIp; j += kThreads) {
-        const uint32_t o = sh.u.lst[j];
-        put_index(bIdx + fI(s) + j, dec_index(o), t.tlo + o);
-      }
-      for (uint32_t j = j0; j < nFp; j += kThreads) {
-        const uint32_t o = sh.u.lst[nIp + j];
-        put_float(j, dec_float(o), o, s, nVp, nLp);
-      }
+  }
+  for (uint32_t p = 0; p < np; ++p) {
+    const uint64_t s = p ? sh.pend[p - 1] : 0, e = p ? sh.pend[p] : pe0;
+    if (p) {  // block-uniform
+      bk.sync();
+      if (mypass == p) build(s, e);
+      bk.sync();
     }
-    // each row's offset: the indices before its label
-    uint64_t rl = eL;
-    for (uint64_t m = so.L; m; m &= m - 1, ++rl) {
-      const uint64_t below = (m & (0 - m)) - 1;
-      if (rl < a.cap[C_ROWS]) a.offset[rl] = eI + popc64(so.I & below);
-      else raise_error(a.err, E_CAPACITY, P + ctz64(m));
+    const uint64_t cn = e - s;
+    const uint32_t nIp = fI(cn), nVp = fV(cn), nLp = fL(cn), nFp = nVp + nLp + fW(cn), fbp = kIW * nIp;
+    const uint32_t j0 = (uint32_t)tid + (p ? 0u : (uint32_t)kB * kThreads);
+    for (uint32_t j = j0; j < nIp; j += kThreads) {
+      const uint32_t o = sh.u.lst[j];
+      put_index(bIdx + fI(s) + j, dec_index(o), t.tlo + o);
     }
+    for (uint32_t j = j0; j < nFp; j += kThreads) {
+      const uint32_t o = sh.u.lst[fbp + j];
+      put_float(j, dec_float(o), o, s, nVp, nLp);
+    }
+    if constexpr (FM)
+      for (uint32_t j = (uint32_t)tid; j < nIp; j += kThreads) put_field(bIdx + fI(s) + j, sh.u.lst[nIp + j]);
+  }
+  // each row's offset: the indices before its label
+  uint64_t rl = eL;
+  for (uint64_t m = so.L; m; m &= m - 1, ++rl) {
+    const uint64_t below = (m & (0 - m)) - 1;
+    if (rl < a.cap[C_ROWS]) a.offset[rl] = eI + popc64(so.I & below);
+    else raise_error(a.err, E_CAPACITY, P + ctz64(m));
+  }
+  if constexpr (!FM) {
     // qid runs (every row has one when this path stands, qid_fix_kernel):
     // row r's id, atoll of its digits (libsvm_parser.h:126-130)
     for (uint64_t m = so.Q; m; m &= m - 1) {
       const uint64_t bit = m & (0 - m), x = P + ctz64(m);
       const uint64_t r = eL + popc64(so.L & (bit - 1)) - 1;  // the row of the label before it
       uint64_t v = 0;
-      for (uint64_t p = x; is_digit(at(p)); ++p) v = v * 10 + (at(p) - '0');
+      for (uint64_t q = x; is_digit(at(q)); ++q) v = v * 10 + (at(q) - '0');
       if (r < a.cap[C_QID]) a.qid[r] = v;
       else raise_error(a.err, E_CAPACITY, x);
     }
   } else {
-    // libfm: the register batch, then the rest of this segment's runs, one
-    // role at a time (no divergence between the index and value decoders)
-    const uint32_t nIm = (uint32_t)popc64(so.I), nFm = (uint32_t)popc64(so.V | so.L | so.W);
-    uint64_t rv = eV, rl = eL, rw = eW;  // this thread's running output ranks
-    auto put_float = [&](uint32_t bpos, float v) {
-      const uint64_t bit = 1ull << bpos, q = P + bpos;
-      if (so.V & bit) {
-        put_value(rv++, v, q);
-      } else if (so.L & bit) {
-        if (rl < a.cap[C_ROWS]) {
-          a.label[rl] = v;
-          a.offset[rl] = eI + popc64(so.I & (bit - 1));
-        } else {
-          raise_error(a.err, E_CAPACITY, q);
-        }
-        ++rl;
-      } else {
-        put_weight(rw++, v, q);
-      }
-    };
-#pragma unroll
-    for (int u = 0; u < kB; ++u) {
-      if ((uint32_t)u < nIm) put_index(eI + u, ib[u], P);
-      if ((uint32_t)u < nFm) put_float((fpos >> (6 * u)) & 63u, fb[u]);
-    }
-    for (uint64_t r = eI + kB; mI; mI &= mI - 1, ++r) {
-      const uint32_t o = (uint32_t)(P - t.tlo) + ctz64(mI);
-      put_index(r, dec_index(o), t.tlo + o);
-    }
-    for (; mF; mF &= mF - 1) {
-      const uint32_t bpos = (uint32_t)ctz64(mF);
-      put_float(bpos, dec_float((uint32_t)(P - t.tlo) + bpos));
-    }
     // every v1 is decoded by the reference: a '-' field is the sign error
     // even when its triple is dropped (strtonum.h:416, libfm_parser.h:104)
     for (uint64_t m = soF; m; m &= m - 1) {
       const uint64_t q = P + ctz64(m);
       if (sh.c.text[q - t.tlo + kPre] == '-') raise_error(a.err, E_NEG_INDEX, q);
-    }
-    // each index's field: the run before it (scanned back over the LDS masks)
-    uint64_t r = eI;
-    for (uint64_t m = so.I; m; m &= m - 1, ++r) {
-      const uint64_t q = P + ctz64(m);
-      const uint64_t f0 = t.floor_of(q);
-      const uint64_t fe = t.last_bit(0, f0, q);
-      const uint64_t x = fe == kNone ? kNone : t.last_bit(1, f0, fe);
-      const uint64_t fs = x == kNone ? f0 : x + 1;
-      const uint64_t lim = lim_of(fs);
-      uint64_t v = 0;
-      bool ok = false, pos = true;
-      if (fs + kPre >= t.tlo && fs + 16 <= lim) {
-        const W16 wq = win_at(sh.c.text, t.tlo, fs);
-        const uint32_t w4[4] = {(uint32_t)wq.lo, (uint32_t)(wq.lo >> 32), (uint32_t)wq.hi, (uint32_t)(wq.hi >> 32)};
-        pos = wuint32(w4, sh.dt, &v, &ok);
-      }
-      if (!ok) pos = slow_uint(a.text, fs, lim, a.wide, &v);
-      if (!pos) v = 0;  // raised by the field's owner above
-      if (a.indexing_mode > 0) --v;
-      if (r < a.cap[C_FIELD]) {
-        if (a.wide) reinterpret_cast<uint64_t *>(a.field)[r] = v;
-        else reinterpret_cast<uint32_t *>(a.field)[r] = (uint32_t)v;
-      } else {
-        raise_error(a.err, E_CAPACITY, q);
-      }
     }
   }
   FAST_STAMP(k, 8);

@@ -127,6 +127,20 @@ def dense_libsvm(rng, nbytes, style):
     return ("\n".join(out) + "\n").encode("latin-1")
 
 
+def dense_libfm(rng, nbytes):
+    """libfm rows of one-digit triples ("l f:i:v f:i:v ..."): several thousand
+    runs per 16 KiB tile, so the libfm run lists (indices, fields, values) take
+    several passes."""
+    out, n = [], 0
+    while n < nbytes:
+        d = lambda: str(int(rng.integers(0, 10)))
+        line = d() + (":" + d() if rng.random() < 0.2 else "") + "".join(
+            " %s:%s:%s" % (d(), d(), d()) for _ in range(int(rng.integers(1, 50))))
+        out.append(line)
+        n += len(line) + 1
+    return ("\n".join(out) + "\n").encode("latin-1")
+
+
 def _csv_field(rng):
     r = rng.random()
     if r < 0.08:

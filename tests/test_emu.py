@@ -189,6 +189,18 @@ def test_emu_fast_qid_vs_oracle():
     assert paths["fast"] >= 20 and paths["exact"] >= 5, paths
 
 
+def test_emu_libfm_dense_runs():
+    """libfm tiles of one-byte runs: index, field and value lists in passes."""
+    rng = np.random.default_rng(93)
+    for it in range(3):
+        data = fuzz_text.dense_libfm(rng, 2 * 16384 + 555)
+        offs = fuzz_text.random_cuts(rng, data, 3, anywhere=False)
+        o = po.parse_chunks(data, offs, fmt=po.LIBFM)
+        h = pyemu.parse(data, offs, "libfm")
+        assert o["status"] == 0 and not check_fail(h, "libfm", offs), o["msg"]
+        assert h["path"] == "fast" and diff(h, o) == []
+
+
 def test_emu_fast_equals_exact_synthetic():
     text, _ = synth.rows(synth.LIBSVM, 800, 40, seed=5)
     data = text.tobytes()

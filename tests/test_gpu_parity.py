@@ -262,6 +262,16 @@ def test_gpu_fast_dense_runs_vs_oracle(dm):
         assert h["path"] == "fast", (it, style)
 
 
+def test_gpu_libfm_dense_runs_vs_oracle(dm):
+    """libfm tiles of one-byte runs: the index, field and value lists in passes."""
+    rng = np.random.default_rng(1313)
+    for it in range(4):
+        data = fuzz_text.dense_libfm(rng, int(rng.integers(3, 30)) * 16384 + int(rng.integers(0, 999)))
+        offs = fuzz_text.random_cuts(rng, data, int(rng.integers(0, 8)), anywhere=False)
+        h = _gpu_vs_oracle_paths(dm, data, offs, fmt=po.LIBFM, **({"index_bits": 64} if it % 2 else {}))
+        assert h["path"] == "fast", it
+
+
 def test_gpu_fast_qid_vs_oracle(dm):
     """"qid:" rows through the single-pass kernel (svm_fast.h qid_clean /
     qid_ok, qid_fix_kernel): fast and exact paths both equal the oracle;
