@@ -31,16 +31,32 @@ using namespace fast;
 // look-back slots: rows, values, the segmented delimiter tail, its row-start flag
 enum { Q_ROWS = 0, Q_VALS = 1, Q_TAIL = 2, Q_FLAG = 3 };
 
+struct Planes {  // slot 0: the segment before the tile; slot t+1: segment t
+  uint64_t d[kThreads + 1];  // number characters
+  uint64_t n[kThreads + 1];  // newlines
+  uint64_t l[kThreads + 1];  // delimiters
+};
+// token list entries (svm_fast.h's run lists for CSV): tile offset (14 bits),
+// column since the row start or the tile start (17 bits: at most kTile
+// delimiters lie before a token in its tile), bit 31: add the carry the
+// look-back brings (the token's row started before the tile)
+constexpr int kListCap = (int)(sizeof(Planes) / sizeof(uint32_t));
+constexpr uint32_t kPassTokens = (uint32_t)kListCap - kSegB;
+constexpr uint32_t kColBits = 17;
+
 struct Shared {  // LDS of one workgroup
   TileCommon c;
-  uint64_t md[kThreads + 1];  // slot 0: the segment before the tile; slot t+1: segment t
-  uint64_t mn[kThreads + 1];
-  uint64_t ml[kThreads + 1];
+  union {
+    Planes m;
+    uint32_t lst[kListCap];
+  } u;
   uint32_t cls[256];  // byte classes: byte 0 number char, 1 digit (without 0: outside the grammar), 2 newline, 3 delimiter
   DecTables dt;
-  uint16_t g16[kThreads + 1];  // digit plane, bytes 0-15 of segment t (t = kThreads: the post-halo)
+  uint32_t gw[2 * kThreads + 2];  // digit plane as words: 2t, 2t+1 segment t; 2 kThreads: the post-halo
   uint64_t segc;      // the tile's segmented carry (delimiters since the last row start before it)
   uint32_t nlab, nfirst;  // label_col >= 0: label tokens / first delimiters of rows in this tile
+  uint32_t pend[kTile / kPassTokens + 2];  // token counts at the end of each pass
+  uint32_t npass;
 };
 
 DA_HD uint32_t class_of_csv(uint32_t b, uint32_t delim) {
@@ -176,7 +192,7 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
   ChunkProbe cp;  // wave 0: the window load stays in flight through classification
   if (tid < kWave) cp = chunk_list_begin(a.cs, a.nchunk, t.tlo, bk);
   if (tid == 0) {
-    sh.md[0] = sh.mn[0] = sh.ml[0] = 0;
+    sh.u.m.d[0] = sh.u.m.n[0] = sh.u.m.l[0] = 0;
     sh.nlab = sh.nfirst = 0;
   }
   sh.cls[tid] = class_of_csv((uint32_t)tid, a.delim);
@@ -186,11 +202,10 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
   // ---- classify: segment tid -> slot tid+1; lanes 0..15 also one dword
   // each of the 64 bytes before the tile -> slot 0
   uint32_t bad = 0;
-  uint64_t G;  // digit plane of my segment: the decoder's digit masks come from it
   {
     const Masks m = classify64_lut(sh.c.text + kPre + tid * kSegB, sh.cls);
-    G = m.g;
-    sh.g16[tid] = (uint16_t)m.g;
+    sh.gw[2 * tid] = (uint32_t)m.g;
+    sh.gw[2 * tid + 1] = (uint32_t)(m.g >> 32);
     if (tid == kWave) {  // digits of the 16 bytes after the tile (windows of my last values)
       uint32_t g = 0;
 #pragma unroll
@@ -199,11 +214,11 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
         memcpy(&x, sh.c.text + kPre + kTile + 4 * i, 4);
         g |= classify_dword_lut(x, sh.cls).g << (4 * i);
       }
-      sh.g16[kThreads] = (uint16_t)g;
+      sh.gw[2 * kThreads] = g;
     }
-    sh.md[tid + 1] = m.d;
-    sh.mn[tid + 1] = m.n;
-    sh.ml[tid + 1] = m.c;
+    sh.u.m.d[tid + 1] = m.d;
+    sh.u.m.n[tid + 1] = m.n;
+    sh.u.m.l[tid + 1] = m.c;
     // bytes past the end of the text are staged as blanks: judge valid bytes only
     const uint64_t P0 = t.tlo + (uint64_t)tid * kSegB;
     const uint64_t vmask = P0 >= a.n ? 0ull : (a.n - P0 >= 64 ? ~0ull : ((1ull << (a.n - P0)) - 1));
@@ -212,9 +227,9 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
       uint32_t x;
       memcpy(&x, sh.c.text + (kPre - kSegB) + 4 * tid, 4);
       const Nib b = classify_dword_lut(x, sh.cls);
-      atomic_or_u64(&sh.md[0], (uint64_t)b.d << (4 * tid));
-      atomic_or_u64(&sh.mn[0], (uint64_t)b.n << (4 * tid));
-      atomic_or_u64(&sh.ml[0], (uint64_t)b.c << (4 * tid));
+      atomic_or_u64(&sh.u.m.d[0], (uint64_t)b.d << (4 * tid));
+      atomic_or_u64(&sh.u.m.n[0], (uint64_t)b.n << (4 * tid));
+      atomic_or_u64(&sh.u.m.l[0], (uint64_t)b.c << (4 * tid));
     }
   }
   if (tid < kWave) chunk_list_end(a.cs, a.nchunk, t.tlo, t.thi, cp, sh.c, bk);
@@ -226,17 +241,17 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
   if (P < a.n) {
     const int nv = (int)mn<uint64_t>(64, a.n - P);
     const uint64_t valid = nv == 64 ? ~0ull : ((1ull << nv) - 1);
-    const uint64_t N = sh.mn[tid + 1];
-    L = sh.ml[tid + 1] & valid;
+    const uint64_t N = sh.u.m.n[tid + 1];
+    L = sh.u.m.l[tid + 1] & valid;
     uint64_t S = 0;  // chunk starts: a "newline before" for the row rule, a field barrier
     for (uint32_t i = 0; i < sh.c.ncs; ++i) {
       const uint64_t x = sh.c.csl[i];
       if (x >= P && x < P + (uint64_t)nv) S |= 1ull << (x - P);
     }
-    const uint64_t nprev = (sh.mn[tid] >> 63) & 1u, lprev = (sh.ml[tid] >> 63) & 1u;
+    const uint64_t nprev = (sh.u.m.n[tid] >> 63) & 1u, lprev = (sh.u.m.l[tid] >> 63) & 1u;
     RS = ~N & valid & ((N << 1) | nprev | S);
     const uint64_t FSd = ((L << 1) | lprev) & ~N & ~S & valid;
-    T = (RS | FSd) & sh.md[tid + 1];
+    T = (RS | FSd) & sh.u.m.d[tid + 1];
   }
   if (bad) atomic_or_u32(&sh.c.bad, 1u);
   // segmented delimiter count of my segment: since my last row start, or all
@@ -265,10 +280,9 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
     if (sh.c.bad) atomic_or_u32(a.gate, 1u);
   }
   const bool one_chunk = sh.c.ncs == 0;
-  const uint64_t Gn = sh.g16[tid + 1];
   auto dec_float = [&](uint64_t q) -> float {
-    const uint32_t b = (uint32_t)(q - P);  // non-digit flags of the window from the digit plane
-    const uint32_t M = ~(uint32_t)((G >> b) | (b ? (Gn << (64u - b)) : 0ull)) & 0xFFFFu;
+    const uint32_t o = (uint32_t)(q - t.tlo);  // non-digit flags of the window from the digit plane
+    const uint32_t M = ~funnel(sh.gw[(o >> 5) + 1], sh.gw[o >> 5], o & 31u);
     const uint64_t lim = one_chunk ? sh.c.cnext : t.next_cs(q);
     bool ok = false;
     float v = 0.f;
@@ -291,7 +305,51 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
   constexpr int kB = FCSV_KB;  // tokens decoded before the look-back
   float vb[kB > 0 ? kB : 1];
   uint64_t mT = T;
-  if (MODE == 2) {
+  const bool has_lab = a.label_col >= 0;
+  // Without a label column the tokens go to an LDS list in output order
+  // (svm_fast.h's run lists): each wave decodes ceil(tokens / 256) values per
+  // thread and consecutive lanes store consecutive values and column ids.  The
+  // list reuses the planes' LDS (the block scan's barriers ordered their last
+  // reads); a tile with more tokens than fit is done in passes.
+  const uint32_t exT = (uint32_t)((ex >> 16) & 0xFFFF);
+  const uint64_t sexl = ex >> 32;  // segmented exclusive delimiter count (flag in bit 31)
+  uint32_t np = 1, mypass = 0, pe0 = nT;
+  auto build = [&](uint32_t s0, uint32_t e0) {  // my tokens into the list of the pass [s0, e0)
+    uint32_t x = exT - s0;
+    const uint32_t o0 = (uint32_t)tid * kSegB;
+    for (uint64_t m = T; m; m &= m - 1) {
+      const uint32_t b = (uint32_t)ctz64(m);
+      const uint64_t below = (1ull << b) - 1, r = RS & (below | (1ull << b));
+      uint32_t col, carried = 0;
+      if (r) {
+        col = (uint32_t)popc64(L & below & (~0ull << (63 - clz64(r))));
+      } else {
+        col = (uint32_t)(sexl & 0x7FFFFFFFu) + (uint32_t)popc64(L & below);
+        carried = (sexl >> 31) ? 0u : 1u;
+      }
+      sh.u.lst[x++] = (o0 + b) | ((col & ((1u << kColBits) - 1)) << 14) | (carried << 31);
+    }
+    (void)e0;
+  };
+  if (MODE == 2 && !has_lab) {
+    if (nT > kPassTokens) {  // block-uniform: several passes
+      const uint32_t own = (uint32_t)popc64(T);
+      mypass = exT / kPassTokens;
+      if (tid == kThreads - 1 || (exT + own) / kPassTokens != mypass) sh.pend[mypass] = exT + own;
+      if (tid == kThreads - 1) sh.npass = mypass + 1;
+      bk.sync();
+      np = sh.npass;
+      pe0 = sh.pend[0];
+    }
+    if (mypass == 0) build(0, pe0);
+    bk.sync();
+#pragma unroll
+    for (int u = 0; u < kB; ++u) {
+      const uint32_t j = (uint32_t)tid + (uint32_t)u * kThreads;
+      vb[u] = 0.f;
+      if (j < pe0) vb[u] = dec_float(t.tlo + (sh.u.lst[j] & 0x3FFFu));
+    }
+  } else if (MODE == 2) {
 #pragma unroll
     for (int u = 0; u < kB; ++u) {
       vb[u] = 0.f;
@@ -317,7 +375,6 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
   // delimiter is the reference's fatal "Delimiter not found",
   // csv_parser.h:128-132), (first delimiters - rows) into labsum; a nonzero
   // sum sets the gate after this kernel and the exact kernels redo the input.
-  const bool has_lab = a.label_col >= 0;
   const uint64_t Lc = has_lab ? (uint64_t)a.label_col : ~0ull;
   const uint64_t eR = bRows + (ex & 0xFFFF), eT = bVal + ((ex >> 16) & 0xFFFF);
   const uint64_t sex = ex >> 32;  // segmented exclusive (flag in bit 31)
@@ -390,7 +447,36 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
       raise_error(a.err, E_CAPACITY, P + b);
     }
   };
-  {
+  if (!has_lab) {
+    // list entry j of the pass starting at token s0: value rank bVal + s0 + j
+    auto put_tok = [&](uint64_t g, uint32_t e, float v) {
+      const uint64_t ci = ((e >> 14) & ((1u << kColBits) - 1)) + ((e >> 31) ? tcarry : 0u);
+      if (g < a.cap[C_VALUE] && g < a.cap[C_INDEX]) {
+        a.value[g] = v;
+        if (a.wide) reinterpret_cast<uint64_t *>(a.index)[g] = ci;
+        else reinterpret_cast<uint32_t *>(a.index)[g] = (uint32_t)ci;
+      } else {
+        raise_error(a.err, E_CAPACITY, t.tlo + (e & 0x3FFFu));
+      }
+    };
+#pragma unroll
+    for (int u = 0; u < kB; ++u) {
+      const uint32_t j = (uint32_t)tid + (uint32_t)u * kThreads;
+      if (j < pe0) put_tok(bVal + j, sh.u.lst[j], vb[u]);
+    }
+    for (uint32_t p = 0; p < np; ++p) {
+      const uint32_t s0 = p ? sh.pend[p - 1] : 0u, e0 = p ? sh.pend[p] : pe0;
+      if (p) {  // block-uniform
+        bk.sync();
+        if (mypass == p) build(s0, e0);
+        bk.sync();
+      }
+      for (uint32_t j = (uint32_t)tid + (p ? 0u : (uint32_t)kB * kThreads); j < e0 - s0; j += kThreads) {
+        const uint32_t e = sh.u.lst[j];
+        put_tok(bVal + s0 + j, e, dec_float(t.tlo + (e & 0x3FFFu)));
+      }
+    }
+  } else {
     uint64_t m = T;
     uint64_t g = eT;
 #pragma unroll

@@ -175,6 +175,25 @@ def uniform_csv(rng, nlines, maxcols=40, delim=",", violate=False):
     return text.encode("latin-1")
 
 
+def dense_csv(rng, nbytes, delim=",", wide=False):
+    """CSV of one-digit fields (some empty): up to 8k tokens per 16 KiB tile,
+    so the CSV token lists (csv_fast.h kPassTokens) take several passes; rows
+    that span tiles carry their column in from the look-back.  wide=True adds
+    a row of more than 2^17 columns (past the list's column field: the exact
+    kernels)."""
+    out, n = [], 0
+    while n < nbytes:
+        ncol = int(rng.integers(1, 4000 if rng.random() < 0.3 else 60))
+        if wide and not out:
+            ncol = (1 << 17) + 300
+        f = rng.integers(0, 11, size=ncol)
+        line = delim.join("" if v == 10 else str(v) for v in f)
+        out.append(line)
+        n += len(line) + 1
+    seps = ["\n"] * 12 + ["\r\n", "\n\n"]
+    return "".join(line + seps[int(rng.integers(0, len(seps)))] for line in out).encode("latin-1")
+
+
 def random_cuts(rng, data, nmax=8, anywhere=False):
     """Chunk offsets: after a newline (as an InputSplit cuts), or, with
     anywhere=True, at arbitrary bytes (the C-ABI allows any chunking)."""

@@ -233,6 +233,22 @@ def test_emu_csv_fast_fuzz_vs_oracle():
     assert fast > 20, fast
 
 
+def test_emu_csv_dense_tokens():
+    """CSV tiles of one-digit fields: the token lists (csv_fast.h) in several
+    passes, rows carried across tiles, a row past 2^17 columns (its tokens'
+    list columns count from the tile start, the look-back adds the rest)."""
+    rng = np.random.default_rng(717)
+    for it in range(4):
+        delim = ",;"[it % 2]
+        data = fuzz_text.dense_csv(rng, 3 * 16384 + 321 if it < 3 else 300000, delim, wide=it == 3)
+        offs = fuzz_text.random_cuts(rng, data, 3, anywhere=False)
+        o = po.parse_chunks(data, offs, fmt=po.CSV, delimiter=delim)
+        h = pyemu.parse(data, offs, "csv", delimiter=delim)
+        assert o["status"] == 0 and not check_fail(h, "csv", offs), o["msg"]
+        assert diff(h, o) == [], (it, diff(h, o)[:3])
+        assert h["path"] == "fast", it
+
+
 def _many_chunks(rng, data, n_cuts, cluster):
     """Chunk starts after newlines, n_cuts of them; plus a dense cluster (>32
     starts inside one 16 KiB tile) so both the 64-ary chunk search (nchunk > 64,

@@ -272,6 +272,19 @@ def test_gpu_libfm_dense_runs_vs_oracle(dm):
         assert h["path"] == "fast", it
 
 
+def test_gpu_csv_dense_tokens_vs_oracle(dm):
+    """CSV tiles of one-digit fields: the token lists in passes (csv_fast.h
+    kPassTokens), rows carried across tiles, a row past 2^17 columns."""
+    rng = np.random.default_rng(1414)
+    for it in range(5):
+        delim = ",;"[it % 2]
+        wide = it == 4
+        data = fuzz_text.dense_csv(rng, 300000 if wide else int(rng.integers(3, 40)) * 16384 + 77, delim, wide=wide)
+        offs = fuzz_text.random_cuts(rng, data, int(rng.integers(0, 8)), anywhere=False)
+        h = _gpu_vs_oracle_paths(dm, data, offs, fmt=po.CSV, delimiter=delim)
+        assert h["path"] == "fast", it
+
+
 def test_gpu_fast_qid_vs_oracle(dm):
     """"qid:" rows through the single-pass kernel (svm_fast.h qid_clean /
     qid_ok, qid_fix_kernel): fast and exact paths both equal the oracle;
