@@ -582,6 +582,7 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
   stage_issue(a.text, a.n, t.tlo, sr, bk);  // text loads first: the chunk search overlaps them
   ChunkProbe cp;  // wave 0: the window load stays in flight through classification
   if (tid < kWave) cp = chunk_list_begin(a.cs, a.nchunk, t.tlo, bk);
+  FAST_STAMP(k, 11);
   if (tid == 0) {
     sh.u.m.d[0] = sh.u.m.n[0] = sh.u.m.c[0] = 0;
     sh.nq = 0;
@@ -641,7 +642,9 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
       atomic_or_u64(&sh.u.m.c[0], bc << (4 * tid));
     }
   }
+  FAST_STAMP(k, 9);
   if (tid < kWave) chunk_list_end(a.cs, a.nchunk, t.tlo, t.thi, cp, sh.c, bk);
+  FAST_STAMP(k, 10);
   bk.sync();
   if (tid == 0) bad |= sh.c.toomany;
   FAST_STAMP(k, 3);

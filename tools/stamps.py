@@ -59,6 +59,11 @@ def main():
             print("  %-14s mean %8.0f cyc  p50 %8.0f  p99 %8.0f" % (PHASES[i], col.mean(), np.median(col),
                                                                    np.percentile(col, 99)))
         print("  total          mean %8.0f cyc" % d.sum(axis=1).mean())
+        if mode == "full":  # sub-phases (thread 0): stage issue / wait; classify compute / chunk list / barrier
+            for name, a0, a1 in (("  stage issue", 1, 11), ("  stage wait+sync", 11, 2), ("  classify body", 2, 9),
+                                 ("  chunk list end", 9, 10), ("  classify barrier", 10, 3)):
+                col = st[:, a1] - st[:, a0]
+                print("  %-18s mean %8.0f cyc  p50 %8.0f" % (name, col.mean(), np.median(col)))
         rounds = st[:, 15]
         print("  look-back rounds: mean %.2f p50 %.0f p99 %.0f max %d"
               % (rounds.mean(), np.median(rounds), np.percentile(rounds, 99), rounds.max()))
