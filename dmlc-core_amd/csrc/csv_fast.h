@@ -96,13 +96,17 @@ DA_HDF uint32_t csv_look_back(uint64_t *lb, uint32_t k, const uint32_t cnt[4], u
   bool done = k == 0;
   while (!done) {
     ++rounds;
-    uint64_t s = 0;
-    uint32_t st = 2;
+    // status word and the three prefix words of predecessor j-1-lane (before
+    // tile 0: an inclusive 0); the prefix stands when all three carry kMark
+    uint64_t s = 0, w[3] = {kMark, kMark, kMark};
     if (lane < j) {
-      s = load_agent_u64(lb + (j - 1 - lane) * 8);
-      st = (uint32_t)(s >> 62);
+      const uint64_t *rec = lb + (j - 1 - lane) * 8;
+      s = load_agent_u64(const_cast<uint64_t *>(rec));
+#pragma unroll
+      for (int i = 0; i < 3; ++i) w[i] = load_agent_u64(const_cast<uint64_t *>(rec) + 1 + i);
     }
-    const uint64_t zero = bk.ballot(st == 0), incl = bk.ballot(st == 2);
+    const bool inc = (w[0] & w[1] & w[2] & kMark) != 0;
+    const uint64_t zero = bk.ballot(!inc && (s >> 62) == 0), incl = bk.ballot(inc);
     const uint32_t fz = zero ? (uint32_t)ctz64(zero) : 64u, fi = incl ? (uint32_t)ctz64(incl) : 64u;
     const uint32_t tagg = fi < fz ? fi : fz;
     const uint64_t mine = lane < tagg ? s : 0ull;
@@ -116,17 +120,10 @@ DA_HDF uint32_t csv_look_back(uint64_t *lb, uint32_t k, const uint32_t cnt[4], u
     }
     done = fi < fz;
     if (done) {
-      if ((uint64_t)fi < j) {
-        if (lane == fi) {
-          const uint64_t *rec = lb + (j - 1 - fi) * 8;
-          for (int i = 0; i < 3; ++i) c.lbw[i] = load_agent_u64(const_cast<uint64_t *>(rec) + 1 + i);
-        }
-        bk.wave_sync();
-        rows += c.lbw[0];
-        vals += c.lbw[1];
-        if (!seg_done) tail += c.lbw[2];
-        bk.wave_sync();
-      }
+      rows += bk.shfl(w[0] & ~kMark, (int)fi);
+      vals += bk.shfl(w[1] & ~kMark, (int)fi);
+      const uint64_t t2 = bk.shfl(w[2] & ~kMark, (int)fi);
+      if (!seg_done) tail += t2;
     } else {
       j -= tagg;
       if (tagg == 0) {
@@ -143,17 +140,12 @@ DA_HDF uint32_t csv_look_back(uint64_t *lb, uint32_t k, const uint32_t cnt[4], u
     c.base[Q_VALS] = vals;
     *segc = tail;
   }
-  const uint64_t packed = (uint64_t)cnt[0] | ((uint64_t)cnt[1] << 15) | ((uint64_t)cnt[2] << 30) |
-                          ((uint64_t)cnt[3] << 45);
   uint64_t *rec = lb + (uint64_t)k * 8;
   if (lane < 3) {
     const uint64_t v = lane == 0 ? rows + cnt[0] : lane == 1 ? vals + cnt[1]
                                                            : (cnt[3] ? (uint64_t)cnt[2] : tail + cnt[2]);
-    store_agent_u64(rec + 1 + lane, v);
+    store_agent_u64(rec + 1 + lane, kMark | v);
   }
-  drain_stores();
-  bk.wave_sync();
-  if (lane == 0) store_agent_u64(rec, kSIncl | packed);
   return rounds;
 }
 
@@ -269,11 +261,9 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
     const uint64_t packed = (uint64_t)cnt4[0] | ((uint64_t)cnt4[1] << 15) | ((uint64_t)cnt4[2] << 30) |
                             ((uint64_t)cnt4[3] << 45);
     if (k == 0) {
-      store_agent_u64(rec + 1, cnt4[0]);
-      store_agent_u64(rec + 2, cnt4[1]);
-      store_agent_u64(rec + 3, cnt4[2]);
-      drain_stores();
-      store_agent_u64(rec, kSIncl | packed);
+      store_agent_u64(rec + 1, kMark | cnt4[0]);
+      store_agent_u64(rec + 2, kMark | cnt4[1]);
+      store_agent_u64(rec + 3, kMark | cnt4[2]);
     } else {
       store_agent_u64(rec, kSAgg | packed);
     }

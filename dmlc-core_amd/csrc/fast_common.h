@@ -693,6 +693,87 @@ DA_HD void drain_stores() {
 #endif
 }
 
+// Inclusive prefixes are tagged words: incl[k][f] = kMark | value, each an
+// untorn 8-byte granule that the launch's memset left 0, so a reader takes
+// a tile's inclusive prefix as soon as all four of its words carry the mark
+// -- no drain between the prefix and a status flag, and the reader polls a
+// predecessor's status word and prefix words in the same round trip.
+constexpr uint64_t kMark = 1ull << 63;
+#ifndef FSVM_LB_DRAIN
+
+// Lane 0: publish this tile's aggregate (tile 0 publishes its inclusive).
+DA_HD void publish_aggregate(uint64_t *lb, uint32_t ntiles, uint32_t k, const uint32_t cnt[4]) {
+  uint64_t *st = lb, *incl = lb + ntiles;
+  if (k == 0) {
+    for (int i = 0; i < 4; ++i) store_agent_u64(incl + i, kMark | cnt[i]);
+  } else {
+    store_agent_u64(st + k, kSAgg | pack4(cnt));
+  }
+}
+
+// Wave 0: decoupled look-back.  Lane l polls predecessor j-1-l: its status
+// word (512 contiguous bytes per wave) and its four prefix words; a round
+// consumes predecessors up to the nearest one with a complete inclusive
+// prefix and stops before the nearest unpublished one.  cnt = this tile's
+// counts (wave uniform).  Ends with c.base[0..3] = exclusive prefixes and
+// publishes the inclusive prefix.  Returns the number of rounds.  The caller
+// synchronises.
+template <class BK>
+DA_HDF uint32_t look_back(uint64_t *lb, uint32_t ntiles, uint32_t k, const uint32_t cnt[4], uint32_t *gate,
+                          TileCommon &c, BK &bk) {
+  const uint32_t lane = bk.tid();
+  uint64_t *st = lb, *incl = lb + ntiles;
+  uint64_t j = k;
+  uint32_t spins = 0, rounds = 0;
+  uint64_t acc[4] = {0, 0, 0, 0};
+  bool done = k == 0;
+  while (!done) {
+    ++rounds;
+    uint64_t s = 0, w[4] = {kMark, kMark, kMark, kMark};  // before tile 0: an inclusive 0
+    if (lane < j) {
+      const uint64_t p = j - 1 - lane;
+      s = load_agent_u64(st + p);
+#pragma unroll
+      for (int f = 0; f < 4; ++f) w[f] = load_agent_u64(incl + p * 4 + f);
+    }
+    const bool inc = (w[0] & w[1] & w[2] & w[3] & kMark) != 0;
+    const uint64_t mi = bk.ballot(inc), mz = bk.ballot(!inc && (s >> 62) == 0);
+    uint64_t D = kWave;  // predecessors that contribute their aggregates
+    bool stop_incl = false;
+    if (mz | mi) {
+      D = (uint64_t)ctz64(mz | mi);
+      stop_incl = (mi >> D) & 1u;
+    }
+    uint32_t part[4] = {0, 0, 0, 0};
+    if (lane < D) {
+#pragma unroll
+      for (int f = 0; f < 4; ++f) part[f] = (uint32_t)((s >> (15 * f)) & 0x7FFFu);
+    }
+#pragma unroll
+    for (int f = 0; f < 4; ++f) acc[f] += bk.wave_sum(part[f]);
+    if (stop_incl) {
+      done = true;
+#pragma unroll
+      for (int f = 0; f < 4; ++f) acc[f] += bk.shfl(w[f] & ~kMark, (int)D);
+    } else {
+      j -= D;
+      if (D == 0) {
+        if (++spins > kSpinLimit) {  // never expected: hand the input to the exact path
+          if (lane == 0) atomic_or_u32(gate, 2u);
+          done = true;
+        }
+        spin_pause();
+      }
+    }
+  }
+  if (lane < 4) {
+    const uint64_t v = acc[lane == 0 ? 0 : lane == 1 ? 1 : lane == 2 ? 2 : 3];
+    c.base[lane] = v;
+    if (k > 0) store_agent_u64(incl + (uint64_t)k * 4 + lane, kMark | (v + cnt[lane == 0 ? 0 : lane == 1 ? 1 : lane == 2 ? 2 : 3]));
+  }
+  return rounds;
+}
+#else  // A/B build: inclusive prefix drained before an inclusive status word (round 2)
 // Lane 0: publish this tile's aggregate (tile 0 publishes its inclusive).
 DA_HD void publish_aggregate(uint64_t *lb, uint32_t ntiles, uint32_t k, const uint32_t cnt[4]) {
   uint64_t *st = lb, *incl = lb + ntiles;
@@ -784,6 +865,9 @@ DA_HDF uint32_t look_back(uint64_t *lb, uint32_t ntiles, uint32_t k, const uint3
   }
   return rounds;
 }
+#endif
+// words of look-back state per tile the launch must zero (status + prefix)
+constexpr uint64_t kLbWords = 5;
 
 }  // namespace fast
 }  // namespace dmlc_amd

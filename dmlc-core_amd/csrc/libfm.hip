@@ -65,7 +65,7 @@ hipError_t launch_libfm(const LibfmArgs &a, const FastSvmArgs &f, bool use_fast,
     return e;  // rows no tile writes are filled by chunk_fixup_kernel
   if (use_fast) {
     if ((e = hipMemsetAsync(f.err, 0xFF, sizeof(uint64_t), s)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(f.lb, 0, (size_t)f.ntiles * sizeof(uint64_t), s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(f.lb, 0, (size_t)f.ntiles * fast::kLbWords * sizeof(uint64_t), s)) != hipSuccess) return e;
     if (phase == kPhaseCount) {
       fm_fast_tile<1><<<f.ntiles, kThreads, 0, s>>>(f);
     } else {

@@ -92,7 +92,7 @@ hipError_t launch_libsvm(const LibsvmArgs &a, const FastSvmArgs &f, bool use_fas
     return e;  // rows no tile writes are filled by chunk_fixup_kernel
   if (use_fast) {
     if ((e = hipMemsetAsync(f.err, 0xFF, sizeof(uint64_t), s)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(f.lb, 0, (size_t)f.ntiles * sizeof(uint64_t), s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(f.lb, 0, (size_t)f.ntiles * fast::kLbWords * sizeof(uint64_t), s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(f.qsum, 0, kLabShards * 8 * sizeof(uint64_t), s)) != hipSuccess) return e;
     if (phase == kPhaseCount) {
       prof_mark(0, s, "svm_fast_tile<1>");
