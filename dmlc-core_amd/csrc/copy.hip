@@ -1,0 +1,57 @@
+// copy.hip -- stream copies between page-locked host memory and HBM by a
+// kernel (the engine's H2D of text batches and D2H of CSR arrays).  One SDMA
+// engine moved ~20 GB/s per copy on the MI355X box; wavefronts reading or
+// writing the host buffer directly keep enough PCIe requests in flight to
+// run the pipeline ~1.3x faster end to end.
+#include <hip/hip_runtime.h>
+
+#include "dmlc_amd.h"
+
+namespace dmlc_amd {
+namespace {
+constexpr int kCopyThreads = 256, kCopyUnroll = 4;  // 16-byte units per thread per round
+constexpr unsigned kCopyMaxBlocks = 2048;
+
+__global__ void __launch_bounds__(kCopyThreads) copy16_kernel(uint4 *__restrict__ dst, const uint4 *__restrict__ src,
+                                                             uint64_t n16) {
+  const uint64_t stride = (uint64_t)gridDim.x * kCopyThreads * kCopyUnroll;
+  for (uint64_t i = (uint64_t)blockIdx.x * kCopyThreads * kCopyUnroll + threadIdx.x; i < n16; i += stride) {
+    uint4 v[kCopyUnroll];
+#pragma unroll
+    for (int u = 0; u < kCopyUnroll; ++u) {  // every load of the round in flight before any store
+      const uint64_t j = i + (uint64_t)u * kCopyThreads;
+      if (j < n16) v[u] = src[j];
+    }
+#pragma unroll
+    for (int u = 0; u < kCopyUnroll; ++u) {
+      const uint64_t j = i + (uint64_t)u * kCopyThreads;
+      if (j < n16) dst[j] = v[u];
+    }
+  }
+}
+
+__global__ void copy_tail_kernel(uint8_t *dst, const uint8_t *src, uint32_t n) {
+  if (threadIdx.x < n) dst[threadIdx.x] = src[threadIdx.x];
+}
+}  // namespace
+}  // namespace dmlc_amd
+
+extern "C" int dmlc_amd_copy(void *dst, const void *src, uint64_t bytes, void *stream) {
+  if (bytes == 0) return DMLC_AMD_OK;
+  if (!dst || !src) return DMLC_AMD_ERR_ARG;
+  const hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15u) != 0)
+    return hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, s) == hipSuccess ? DMLC_AMD_OK : DMLC_AMD_ERR_HIP;
+  const uint64_t n16 = bytes >> 4;
+  if (n16) {
+    const uint64_t per_block = (uint64_t)dmlc_amd::kCopyThreads * dmlc_amd::kCopyUnroll;
+    const unsigned blocks = (unsigned)std::min<uint64_t>((n16 + per_block - 1) / per_block, dmlc_amd::kCopyMaxBlocks);
+    dmlc_amd::copy16_kernel<<<blocks, dmlc_amd::kCopyThreads, 0, s>>>(
+        static_cast<uint4 *>(dst), static_cast<const uint4 *>(src), n16);
+  }
+  const uint32_t tail = (uint32_t)(bytes & 15u);
+  if (tail)
+    dmlc_amd::copy_tail_kernel<<<1, 64, 0, s>>>(static_cast<uint8_t *>(dst) + (n16 << 4),
+                                                static_cast<const uint8_t *>(src) + (n16 << 4), tail);
+  return hipGetLastError() == hipSuccess ? DMLC_AMD_OK : DMLC_AMD_ERR_HIP;
+}

@@ -343,6 +343,7 @@ struct EngineConfig {
   int depth = 0;             // parsed batches ahead of the consumer (0: 2 per worker)
   bool max_index = false;    // reduce index/field maxima on the device (RowBlockIter::NumCol)
   bool stats = false;        // DMLC_AMD_STATS=1: per-stage times on stderr when the parser ends
+  bool kernel_copy = true;   // H2D / D2H by dmlc_amd_copy (DMLC_AMD_COPY=dma: hipMemcpyAsync)
 
   // batch size, devices and workers from the environment
   // (DMLC_AMD_BATCH_BYTES, DMLC_AMD_DEVICES = "0,1,..." | "all", DMLC_AMD_WORKERS)
@@ -350,6 +351,11 @@ struct EngineConfig {
     batch_bytes = env_bytes("DMLC_AMD_BATCH_BYTES", batch_bytes, 1u << 20);
     if (const char *w = std::getenv("DMLC_AMD_WORKERS")) per_device = std::max(1, std::atoi(w));
     if (const char *st = std::getenv("DMLC_AMD_STATS")) stats = std::atoi(st) != 0;
+    if (const char *c = std::getenv("DMLC_AMD_COPY")) {
+      const std::string v(c);
+      if (v != "dma" && v != "kernel") throw dmlc::Error("DMLC_AMD_COPY: expected dma or kernel, got " + v);
+      kernel_copy = v == "kernel";
+    }
     if (const char *d = std::getenv("DMLC_AMD_DEVICES")) {
       devices.clear();
       int n = 0;
@@ -626,7 +632,7 @@ class HipTextParser : public dmlc::Parser<IndexType, DType> {
     if (st && !w->ev[0])
       for (auto &e : w->ev) hip_check(hipEventCreate(&e), "hipEventCreate");
     if (st) hip_check(hipEventRecord(w->ev[0], s), "hipEventRecord");
-    hip_check(hipMemcpyAsync(d_text, b->text.p, b->bytes, hipMemcpyHostToDevice, s), "H2D text");
+    H2D(d_text, b->text.p, b->bytes, s);
     hip_check(hipMemcpyAsync(d_cs, b->starts.p, (nch + 1) * 8, hipMemcpyHostToDevice, s), "H2D chunk starts");
     if (st) hip_check(hipEventRecord(w->ev[1], s), "hipEventRecord");
     dmlc_amd_params p = cfg_.prm;
@@ -660,9 +666,7 @@ class HipTextParser : public dmlc::Parser<IndexType, DType> {
       b->fail_unit = SIZE_MAX;
     }
     // the CSR into the batch's pinned arrays
-    auto d2h = [&](void *dst, const void *src, size_t bytes) {
-      if (bytes) hip_check(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s), "D2H");
-    };
+    auto d2h = [&](void *dst, const void *src, size_t bytes) { D2H(dst, src, bytes, s); };
     d2h(b->off.reserve(c[DMLC_AMD_ROWS] + 1), out.offset, (c[DMLC_AMD_ROWS] + 1) * 8);
     d2h(b->label.reserve(c[DMLC_AMD_LABEL] + 1), out.label, c[DMLC_AMD_LABEL] * sizeof(DType));
     d2h(b->weight.reserve(c[DMLC_AMD_WEIGHT] + 1), out.weight, c[DMLC_AMD_WEIGHT] * 4);
@@ -684,6 +688,20 @@ class HipTextParser : public dmlc::Parser<IndexType, DType> {
       stat_ns_[S_BUILD] += clk.ns();
       ++stat_batches_;
     }
+  }
+
+  // Bulk copies between the batch's page-locked arrays and HBM: by kernel
+  // (dmlc_amd_copy) unless DMLC_AMD_COPY=dma; one SDMA engine per copy
+  // capped the pipeline
+  void H2D(void *dst, const void *src, size_t bytes, hipStream_t s) {
+    if (!bytes) return;
+    if (cfg_.kernel_copy) CheckRc(dmlc_amd_copy(dst, src, bytes, s));
+    else hip_check(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s), "H2D");
+  }
+  void D2H(void *dst, const void *src, size_t bytes, hipStream_t s) {
+    if (!bytes) return;
+    if (cfg_.kernel_copy) CheckRc(dmlc_amd_copy(dst, src, bytes, s));
+    else hip_check(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s), "D2H");
   }
 
   void Outputs(Worker *w, const uint64_t *want, dmlc_amd_csr *out) {

@@ -8,8 +8,11 @@
 
 #include <cerrno>
 #include <algorithm>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
+#include <mutex>
 #include <regex>
 #include <sstream>
 #include <thread>
@@ -188,9 +191,86 @@ bool TextSplit::OpenAt(size_t file, uint64_t pos) {
   return true;
 }
 
+// Process-wide pool of reader threads (started once, never joined: no thread
+// work at process exit).  ReadAt hands each a piece of a chunk; spawning and
+// joining threads per 8 MiB chunk cost a fifth of the read time.
+namespace {
+class ReadPool {
+ public:
+  static ReadPool &get() {
+    static ReadPool *p = new ReadPool();
+    return *p;
+  }
+  size_t size() const { return nthreads_; }
+  // run fn(0..n-1), piece 0 on the caller; rethrows the first error
+  void run(size_t n, const std::function<void(size_t)> &fn) {
+    std::unique_lock<std::mutex> job(job_mu_);  // one ReadAt at a time uses the pool
+    std::string err;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      fn_ = &fn;
+      err_ = &err;
+      next_ = 1;
+      end_ = n;
+      pending_ = n - 1;
+      ++gen_;
+    }
+    cv_.notify_all();
+    try {
+      fn(0);
+    } catch (const std::exception &e) {
+      std::lock_guard<std::mutex> lk(mu_);
+      if (err.empty()) err = e.what();
+    }
+    std::unique_lock<std::mutex> lk(mu_);
+    done_cv_.wait(lk, [&] { return pending_ == 0; });
+    fn_ = nullptr;
+    if (!err.empty()) throw dmlc::Error(err);
+  }
+
+ private:
+  ReadPool() {
+    const char *e = std::getenv("DMLC_AMD_READ_THREADS");
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    nthreads_ = (size_t)std::min<unsigned>(e ? std::max(1, std::atoi(e)) : 8u, hw);
+    for (size_t i = 1; i < nthreads_; ++i) std::thread([this] { loop(); }).detach();
+  }
+  void loop() {
+    uint64_t seen = 0;
+    std::unique_lock<std::mutex> lk(mu_);
+    for (;;) {
+      cv_.wait(lk, [&] { return gen_ != seen && next_ < end_; });
+      seen = gen_;
+      while (next_ < end_) {
+        const size_t i = next_++;
+        const std::function<void(size_t)> *fn = fn_;
+        std::string *err = err_;
+        lk.unlock();
+        std::string what;
+        try {
+          (*fn)(i);
+        } catch (const std::exception &e) {
+          what = e.what();
+        }
+        lk.lock();
+        if (!what.empty() && err->empty()) *err = what;
+        if (--pending_ == 0) done_cv_.notify_all();
+      }
+    }
+  }
+  size_t nthreads_ = 1;
+  std::mutex job_mu_, mu_;
+  std::condition_variable cv_, done_cv_;
+  const std::function<void(size_t)> *fn_ = nullptr;
+  std::string *err_ = nullptr;
+  size_t next_ = 0, end_ = 0, pending_ = 0;
+  uint64_t gen_ = 0;
+};
+}  // namespace
+
 // len bytes of the open file at pos (all present: the size was taken at
-// construction).  Large reads are split over threads: one core copies page
-// cache at a fraction of what the host's memory system moves.
+// construction).  Large reads are split over the read pool: one core copies
+// page cache at a fraction of what the host's memory system moves.
 void TextSplit::ReadAt(char *buf, size_t len, uint64_t pos) {
   auto span = [this](char *b, size_t n, uint64_t at) {
     while (n) {
@@ -202,32 +282,17 @@ void TextSplit::ReadAt(char *buf, size_t len, uint64_t pos) {
     }
   };
   constexpr size_t kMinSplit = 1u << 20;
-  static const size_t kThreadsMax = [] {
-    const char *e = std::getenv("DMLC_AMD_READ_THREADS");
-    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-    return (size_t)std::min<unsigned>(e ? std::max(1, std::atoi(e)) : 8u, hw);
-  }();
-  const size_t nt = std::min<size_t>(kThreadsMax, len / kMinSplit);
+  ReadPool &pool = ReadPool::get();
+  const size_t nt = std::min<size_t>(pool.size(), len / kMinSplit);
   if (nt <= 1) {
     span(buf, len, pos);
     return;
   }
   const size_t per = (len + nt - 1) / nt;
-  std::vector<std::thread> th;
-  std::string err;
-  for (size_t i = 1; i < nt; ++i) {
-    const size_t o = i * per, n = std::min(per, len - o);
-    th.emplace_back([&, o, n] {
-      try {
-        span(buf + o, n, pos + o);
-      } catch (const std::exception &e) {
-        err = e.what();
-      }
-    });
-  }
-  span(buf, std::min(per, len), pos);
-  for (auto &t : th) t.join();
-  if (!err.empty()) throw dmlc::Error(err);
+  pool.run(nt, [&](size_t i) {
+    const size_t o = i * per;
+    if (o < len) span(buf + o, std::min(per, len - o), pos + o);
+  });
 }
 
 // Bytes from `pos` in `file` to the next record start: past the first newline

@@ -72,6 +72,8 @@ def lib():
                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                             ctypes.c_void_p]
         L.dmlc_amd_last_hip_error.restype = ctypes.c_char_p
+        L.dmlc_amd_copy.restype = ctypes.c_int
+        L.dmlc_amd_copy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
         L.dmlc_amd_profile_begin.restype = ctypes.c_int
         L.dmlc_amd_profile_end.restype = ctypes.c_int
         L.dmlc_amd_profile_end.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int),
@@ -94,7 +96,8 @@ def profile_end():
 
 EXPORTED_SYMBOLS = ("dmlc_amd_parse", "dmlc_amd_workspace_bytes", "dmlc_amd_error_string",
                     "dmlc_amd_device_count", "dmlc_amd_abi_version", "dmlc_amd_strtof_batch",
-                    "dmlc_amd_profile_begin", "dmlc_amd_profile_end", "dmlc_amd_last_hip_error")
+                    "dmlc_amd_profile_begin", "dmlc_amd_profile_end", "dmlc_amd_last_hip_error",
+                    "dmlc_amd_copy")
 
 
 def make_params(fmt="libsvm", index_bits=32, value_type="f32", indexing_mode=0, label_column=-1,

@@ -140,6 +140,13 @@ int dmlc_amd_parse(const void *d_text, uint64_t nbytes, const uint64_t *d_chunk_
 int dmlc_amd_strtof_batch(const void *d_text, const uint64_t *d_offsets, uint64_t n, float *d_out,
                           uint32_t *d_consumed, uint32_t *d_nan_error, void *stream);
 
+/* Stream copy of `bytes` between page-locked host memory (hipHostMalloc) and
+ * device memory, or device to device, by a kernel instead of the DMA engine
+ * (the host side of a parse pipeline: text batches in, CSR arrays out).  Both
+ * pointers must be device-accessible; unaligned pointers fall back to
+ * hipMemcpyAsync.  Asynchronous on `stream`. */
+int dmlc_amd_copy(void *dst, const void *src, uint64_t bytes, void *stream);
+
 /* Kernel timing for benchmarks: between profile_begin and profile_end, every
  * dmlc_amd_parse on this thread brackets its dominant kernel (the single-pass
  * kernel, or the exact write kernel) with HIP events on its stream.

@@ -706,3 +706,23 @@ def test_gpu_valve_hand_over_vs_oracle(dm):
         assert e["split_path"] & 2 and e["full_path"] & 2, e  # the valve fired in the write pass
         assert e["split_error"] == 0 and e["full_error"] == 0, e
         assert e["split_diff"] == [] and e["full_diff"] == [], e
+
+
+@pytest.mark.parametrize("nbytes,shift", [(10_000_007, 0), (4096, 0), (15, 0), (1 << 20, 3)])
+def test_gpu_kernel_copy_host_device(dm, nbytes, shift):
+    """dmlc_amd_copy (the engine's H2D / D2H): page-locked host <-> HBM byte for
+    byte, odd sizes through the tail kernel, unaligned pointers through the
+    hipMemcpyAsync fallback."""
+    import torch
+    L = dm.lib()
+    rng = np.random.default_rng(nbytes)
+    src = torch.from_numpy(rng.integers(0, 256, nbytes + shift, dtype=np.uint8)).pin_memory()
+    dev = torch.zeros(nbytes + 16, dtype=torch.uint8, device="cuda")
+    back = torch.zeros(nbytes + shift, dtype=torch.uint8).pin_memory()
+    s = torch.cuda.current_stream().cuda_stream
+    assert L.dmlc_amd_copy(dev.data_ptr(), src.data_ptr() + shift, nbytes, s) == 0
+    assert L.dmlc_amd_copy(back.data_ptr() + shift, dev.data_ptr(), nbytes, s) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(dev[:nbytes].cpu(), src[shift:])
+    assert int(dev[nbytes:].sum()) == 0  # nothing past the end
+    assert torch.equal(back[shift:], src[shift:])
