@@ -626,7 +626,7 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
     sh.u.m.d[tid + 1] = m.d;
     sh.u.m.n[tid + 1] = m.n;
     sh.u.m.c[tid + 1] = m.c;
-    bad = m.bad;
+    bad |= m.bad;
     if (tid < 16 && t.tlo > 0) {
       uint32_t x;
       memcpy(&x, sh.c.text + (kPre - kSegB) + 4 * tid, 4);

@@ -350,3 +350,24 @@ def test_emu_filldata_goldens(case):
     exp = {k: dec(v) for k, v in case["expect"].items()}
     assert diff(h, exp) == []
     assert blocks_of(h) == case["blocks"]
+
+
+QID_LETTER_FORMS = ["1 dqi:5 3:4\n", "1 iq:5 3:4\n", "1 qi 3:4\n", "1 d 2:3\n", "1 qid:7 3:4\n",
+                    "1 qidd:7 3:4\n", "1 q 2:3:4\n", "1 2:3:4 d\n", "1 qqid:3 2:1\n", "1:2 idq:4 5:6\n"]
+
+
+@pytest.mark.parametrize("fmt", ["libsvm", "libfm"])
+def test_emu_qid_letter_forms(fmt):
+    """Letters of "qid" that do not spell a "qid:" token (svm_fast.h qid_clean
+    reports them) leave the single-pass grammar: the reference's result or its
+    error, never a role read off blanked letters."""
+    f = {"libsvm": po.LIBSVM, "libfm": po.LIBFM}[fmt]
+    for line in QID_LETTER_FORMS:
+        for data in (line, "0 1:1\n" * 700 + line + "0 1:1\n" * 300):  # one tile / mid-file
+            offs = [0, len(data)]
+            o = po.parse_chunks(data, offs, fmt=f)
+            h = pyemu.parse(data, offs, fmt)
+            failed = check_fail(h, fmt, offs)
+            assert (o["status"] != 0) == failed, (fmt, line, o["msg"], h["error"])
+            if not failed:
+                assert diff(h, o) == [], (fmt, line, diff(h, o))

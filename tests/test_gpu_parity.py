@@ -726,3 +726,15 @@ def test_gpu_kernel_copy_host_device(dm, nbytes, shift):
     assert torch.equal(dev[:nbytes].cpu(), src[shift:])
     assert int(dev[nbytes:].sum()) == 0  # nothing past the end
     assert torch.equal(back[shift:], src[shift:])
+
+
+@pytest.mark.parametrize("fmt", [po.LIBSVM, po.LIBFM])
+def test_gpu_qid_letter_forms_vs_oracle(dm, fmt):
+    """Letters of "qid" that spell no "qid:" token leave the single-pass
+    grammar (svm_fast.h qid_clean's verdict is kept): the reference's result
+    or its error, in a one-line input and in the middle of a multi-tile file."""
+    lines = ["1 dqi:5 3:4\n", "1 iq:5 3:4\n", "1 qi 3:4\n", "1 d 2:3\n", "1 qid:7 3:4\n",
+             "1 qidd:7 3:4\n", "1 q 2:3:4\n", "1 2:3:4 d\n", "1 qqid:3 2:1\n", "1:2 idq:4 5:6\n"]
+    for line in lines:
+        for data in (line, "0 1:1\n" * 7000 + line + "0 1:1\n" * 3000):
+            _gpu_vs_oracle_paths(dm, data, [0, len(data)], fmt=fmt)
