@@ -105,7 +105,8 @@ struct Shared {  // LDS of one workgroup
   uint32_t gw[2 * kThreads + 2];  // digit plane as words: 2t, 2t+1 segment t; 2 kThreads: the post-halo
   uint64_t pend[kTile / kPassRuns + 2];  // packed inclusive counts at the end of each pass
   uint32_t npass;
-  uint32_t nq;  // qid runs of the tile
+  uint32_t nq;     // qid runs of the tile
+  uint32_t hashy;  // a byte outside the grammar: comments to blank (pass 1)
 };
 
 struct Tile {
@@ -259,6 +260,149 @@ DA_HD bool carry_fast(uint64_t d1, uint64_t n1r, uint64_t c1r, uint32_t *dc, uin
   const uint64_t gm = ((1ull << qb) - 1) & ~((2ull << p2) - 1);
   *prole = (n1 & gm) ? R_L : (q1 & gm) ? R_Q : ((c1 & gm) ? R_K : R_I);
   return true;
+}
+
+// ---- '#' comments (libsvm_parser.h:67-83 IgnoreCommentAndBlank) in the fast
+// grammar.  Where the reference calls IgnoreCommentAndBlank -- the line start
+// and every pair end -- a '#' that is the first non-blank byte drops the rest
+// of the line.  In the uniform grammar a pair end is the end of any digitchar
+// run (ParsePair's endptr, strtonum.h:667-703), so a '#' whose nearest
+// non-blank predecessor in the line is a run or the line start opens a
+// comment; one after a ':' or a "qid:" token does not, and after the comment
+// is blanked that ':' dangles at the line end (or the token lacks its digit),
+// which the role checks already send to the exact kernels.
+//
+// So a comment is "from a '#' to the next newline or range start", found with
+// the carry trick: X = bytes that do not end a comment, seeds A = '#' bytes;
+// in X + A + cin a carry enters every byte of a run of X after its first seed
+// (or from bit 0 when a comment is open before the segment), so the comment
+// bytes are X & (A | carries), carries = (X + A + cin) ^ X ^ A.  Segments compose by the
+// function (open before -> open after), two bits, by one block scan.  The
+// tile's comment bytes -- and those of the staged halos -- become blanks in
+// the LDS text and classification runs again; the tile start's state comes
+// from the pre-halo alone (a comment open there has its '#' in the pre-halo),
+// which the tile before checks: a comment open at its end whose '#' lies
+// further back than the next tile's pre-halo raises the gate.
+// A '#' opens a comment when the bytes between it and the previous digitchar
+// (a pair end) or range start are blanks: "reachable" bytes.  A line start
+// after a newline is not one -- ParseBlock's line begins at the previous
+// line's '\n' (libsvm_parser.h:91-96), which IgnoreCommentAndBlank does not
+// skip, so there ParsePair reads the '#' line's digits as the label and the
+// exact kernels take it.
+struct CmtBlock {
+  uint64_t A, B;  // comment-opening '#', comment ends
+  uint32_t rout;  // the byte after the block is reachable
+  uint32_t free_;  // all blanks, no range start: rout = the block's reach-in
+};
+// the 64 staged bytes at p; S: range starts among them; r: reach-in
+DA_HD CmtBlock comment_block(const uint8_t *p, uint64_t S, uint32_t r) {
+  uint64_t h = 0, nl = 0, bl = 0, dg = 0;
+#pragma unroll 4
+  for (int i = 0; i < 64; ++i) {
+    const uint32_t b = p[i];
+    h |= (uint64_t)(b == '#') << i;
+    nl |= (uint64_t)is_nl(b) << i;
+    bl |= (uint64_t)is_blank(b) << i;
+    dg |= (uint64_t)is_digitchar(b) << i;
+  }
+  const uint64_t ok = (dg << 1) | S, seeds = ok & bl;
+  uint32_t ro;
+  const uint64_t reach = ok | (add_carry(bl, seeds, r, &ro) ^ bl ^ seeds);
+  CmtBlock o;
+  o.A = h & reach;
+  o.B = nl | (S & ~o.A);  // a range start ends a comment, unless it opens one
+  o.rout = ro | (uint32_t)(dg >> 63);
+  o.free_ = (~bl == 0) && S == 0;
+  return o;
+}
+// open-after as a function of open-before: bit 0 = f(0), bit 1 = f(1)
+DA_HD uint32_t comment_fn(uint64_t A, uint64_t B) {
+  uint32_t o0, o1;
+  (void)add_carry(~B, A, 0u, &o0);
+  (void)add_carry(~B, A, 1u, &o1);
+  return o0 | (o1 << 1);
+}
+struct CommentFnCompose {  // a then b
+  DA_HD uint32_t operator()(uint32_t a, uint32_t b) const {
+    return ((b >> (a & 1u)) & 1u) | (((b >> ((a >> 1) & 1u)) & 1u) << 1);
+  }
+};
+// blank the bytes of mask m in the 64 staged bytes at p
+DA_HD void blank_bytes(uint8_t *p, uint64_t m) {
+  for (; m; m &= m - 1) p[ctz64(m)] = ' ';
+}
+// the comment bytes of a segment (A '#', B comment ends, cin open before it);
+// *co: open after it
+DA_HD uint64_t comment_mask(uint64_t A, uint64_t B, uint32_t cin, uint32_t *co) {
+  const uint64_t X = ~B;
+  return X & (A | (add_carry(X, A, cin, co) ^ X ^ A));
+}
+// chunk starts in [lo, lo + 64) as bits (the tile's list and the one after it)
+DA_HD uint64_t cs_bits(const TileCommon &c, uint64_t lo) {
+  uint64_t s = 0;
+  for (uint32_t i = 0; i <= c.ncs; ++i) {
+    const uint64_t x = i < c.ncs ? c.csl[i] : c.cnext;
+    if (x >= lo && x < lo + 64) s |= 1ull << (x - lo);
+  }
+  if (c.cfloor >= lo && c.cfloor < lo + 64) s |= 1ull << (c.cfloor - lo);
+  return s;
+}
+// Blanks the comments of the staged text (pre-halo, tile, post-halo); all
+// threads.  Returns 1 (gate) when the tile after this one cannot see from its
+// pre-halo that a comment is open at its start.
+template <class BK>
+DA_HDF uint32_t comment_erase(uint64_t tlo, uint64_t thi, uint64_t n, TileCommon &c, BK &bk) {
+  const int tid = bk.tid();
+  uint8_t *txt = c.text;
+  auto block_at = [&](int j, uint32_t r) {  // segment j of the tile, -1 the pre-halo
+    return comment_block(txt + kPre + j * kSegB, cs_bits(c, tlo + (int64_t)j * kSegB), r);
+  };
+  // the tile start: a comment open at the end of the pre-halo, the pre-halo
+  // read on its own (reach-in 0), as the tile before checks it
+  CmtBlock h{0, 0, 0, 0};
+  uint32_t c0 = 0;
+  if (tlo > 0) {
+    h = block_at(-1, 0u);
+    c0 = comment_fn(h.A, h.B) & 1u;
+  }
+  // reach-in: back over the staged bytes to the first block that decides it
+  uint32_t r = 0;
+  for (int j = tid - 1; j >= (tlo > 0 ? -1 : 0); --j) {
+    const CmtBlock b = block_at(j, 0u);
+    if (!b.free_ || j == -1) {
+      r = b.rout;
+      break;
+    }
+  }
+  const uint64_t P = tlo + (uint64_t)tid * kSegB;
+  const CmtBlock m = block_at(tid, r);
+  const uint32_t f = comment_fn(m.A, m.B);
+  // the next tile reads the state at its start from its pre-halo (this
+  // segment) alone, reach-in 0
+  uint32_t f_next = 0;
+  if (tid == kThreads - 1) {
+    const CmtBlock nx = block_at(tid, 0u);
+    f_next = comment_fn(nx.A, nx.B) & 1u;
+  }
+  uint32_t tot;
+  const uint32_t pre = bk.exclusive(f, 2u, CommentFnCompose(), &tot);  // (its barriers order the reads above)
+  const uint32_t cin = (pre >> c0) & 1u;
+  uint32_t co, gate = 0;
+  blank_bytes(txt + kPre + tid * kSegB, comment_mask(m.A, m.B, cin, &co));
+  if (tid == 0 && tlo > 0) {
+    uint32_t ch;
+    blank_bytes(txt, comment_mask(h.A, h.B, 0u, &ch));
+  }
+  if (tid == kThreads - 1) {
+    if (thi < n && P + kSegB == thi && !(cs_bits(c, thi) & 1u) && co != f_next) gate = 1;
+    uint32_t ci = co, ri = m.rout;
+    for (int s = 0; s < kPost / kSegB; ++s) {
+      const CmtBlock b = block_at(kThreads + s, ri);
+      blank_bytes(txt + kPre + kTile + s * kSegB, comment_mask(b.A, b.B, ci, &ci));
+      ri = b.rout;
+    }
+  }
+  return gate;
 }
 
 // Runs, roles and counts of segment tid (positions P .. P+63).
@@ -559,6 +703,70 @@ FSVM_COLD bool slow_uint(const uint8_t *text, uint64_t q, uint64_t lim, int wide
   return parse_uint(src, q, wide != 0, v);
 }
 
+// Classification of segment tid (and, lanes 0..15, of the pre-halo): the LDS
+// planes, the digit-plane words; returns the segment's grammar flag.  `first`:
+// pass 0, which also notes bytes outside the grammar (sh.hashy).
+template <bool FM, class At>
+DA_HDF uint32_t classify_tile(const Tile &t, Shared &sh, int tid, At at, bool first) {
+  uint32_t bad = 0;
+  Masks m = classify64_lut(sh.c.text + kPre + tid * kSegB, sh.cls);
+  const uint64_t P0 = t.tlo + (uint64_t)tid * kSegB;
+  if ((m.n & m.c) || ((m.c & 1) && P0 > 0 && is_qid_letter(at(P0 - 1)))) {  // letters: "qid:" tokens
+    if (FM || !qid_clean(P0, &m.n, &m.c, P0 > 0 && is_qid_letter(at(P0 - 1)), at)) bad = 1;
+  }
+  sh.gw[2 * tid] = (uint32_t)m.g;
+  sh.gw[2 * tid + 1] = (uint32_t)(m.g >> 32);
+  if (tid == kWave) {  // digits of the 16 bytes after the tile (windows of my last runs)
+    uint32_t g = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      uint32_t x;
+      memcpy(&x, sh.c.text + kPre + kTile + 4 * i, 4);
+      g |= classify_dword_lut(x, sh.cls).g << (4 * i);
+    }
+    sh.gw[2 * kThreads] = g;
+  }
+  sh.u.m.d[tid + 1] = m.d;
+  sh.u.m.n[tid + 1] = m.n;
+  sh.u.m.c[tid + 1] = m.c;
+  bad |= m.bad;
+  if (!FM && first && m.bad) sh.hashy = 1;
+  if (tid < 16 && t.tlo > 0) {
+    uint32_t x;
+    memcpy(&x, sh.c.text + (kPre - kSegB) + 4 * tid, 4);
+    const Nib b = classify_dword_lut(x, sh.cls);
+    if (!FM && first && b.bad) sh.hashy = 1;
+    uint64_t bn = b.n, bc = b.c;
+    const uint64_t P0 = t.tlo - kSegB + 4 * tid;
+    if (!FM && ((bn & bc) || (bc & 1))) {  // the bytes' owner tile checks them; here only their planes
+      const bool lead = is_qid_letter(at(P0 - 1));
+      if ((bn & bc) || lead) (void)qid_clean(P0, &bn, &bc, lead, at);
+    }
+    atomic_or_u64(&sh.u.m.d[0], (uint64_t)b.d << (4 * tid));
+    atomic_or_u64(&sh.u.m.n[0], bn << (4 * tid));
+    atomic_or_u64(&sh.u.m.c[0], bc << (4 * tid));
+  }
+  return bad;
+}
+
+// Pass 1 (libsvm): blank the comments, classify again; all threads, after the
+// chunk list is known.  Returns the segment's grammar flag.
+template <class BK>
+DA_HDF uint32_t comments_reclassify(const Tile t, Shared &sh, BK &bk) {
+  const int tid = bk.tid();
+  const FastSvmArgs &a = *t.a;
+  const uint32_t cgate = comment_erase(t.tlo, t.thi, a.n, sh.c, bk);
+  if (tid == 0) sh.u.m.d[0] = sh.u.m.n[0] = sh.u.m.c[0] = 0;
+  bk.sync();
+  auto at = [&](uint64_t p) -> uint32_t {
+    if (p >= a.n) return 0u;
+    return p + kPre >= t.tlo ? (uint32_t)sh.c.text[p - t.tlo + kPre] : (uint32_t)a.text[p];
+  };
+  const uint32_t bad = classify_tile<false>(t, sh, tid, at, false);
+  bk.sync();
+  return bad | cgate;
+}
+
 // MODE 1: count only (size query); MODE 2: parse and write.
 template <int MODE, bool FM = false, class BK>
 DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
@@ -586,6 +794,7 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
   if (tid == 0) {
     sh.u.m.d[0] = sh.u.m.n[0] = sh.u.m.c[0] = 0;
     sh.nq = 0;
+    sh.hashy = 0;
   }
   sh.cls[tid] = class_of((uint32_t)tid);
   init_dec_tables(sh.dt, bk);
@@ -598,54 +807,20 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
 #endif
   // ---- classify: segment tid -> slot tid+1; lanes 0..15 also one word each
   // of the 64 bytes before the tile -> slot 0
-  uint32_t bad = 0;
   // a text byte (0 outside the text) for the qid token checks: staged, or
   // from global memory before the staged bytes
   auto at = [&](uint64_t p) -> uint32_t {
     if (p >= a.n) return 0u;
     return p + kPre >= t.tlo ? (uint32_t)sh.c.text[p - t.tlo + kPre] : (uint32_t)a.text[p];
   };
-  {
-    Masks m = classify64_lut(sh.c.text + kPre + tid * kSegB, sh.cls);
-    const uint64_t P0 = t.tlo + (uint64_t)tid * kSegB;
-    if ((m.n & m.c) || ((m.c & 1) && P0 > 0 && is_qid_letter(at(P0 - 1)))) {  // letters: "qid:" tokens
-      if (FM || !qid_clean(P0, &m.n, &m.c, P0 > 0 && is_qid_letter(at(P0 - 1)), at)) bad = 1;
-    }
-    sh.gw[2 * tid] = (uint32_t)m.g;
-    sh.gw[2 * tid + 1] = (uint32_t)(m.g >> 32);
-    if (tid == kWave) {  // digits of the 16 bytes after the tile (windows of my last runs)
-      uint32_t g = 0;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        uint32_t x;
-        memcpy(&x, sh.c.text + kPre + kTile + 4 * i, 4);
-        g |= classify_dword_lut(x, sh.cls).g << (4 * i);
-      }
-      sh.gw[2 * kThreads] = g;
-    }
-    sh.u.m.d[tid + 1] = m.d;
-    sh.u.m.n[tid + 1] = m.n;
-    sh.u.m.c[tid + 1] = m.c;
-    bad |= m.bad;
-    if (tid < 16 && t.tlo > 0) {
-      uint32_t x;
-      memcpy(&x, sh.c.text + (kPre - kSegB) + 4 * tid, 4);
-      const Nib b = classify_dword_lut(x, sh.cls);
-      uint64_t bn = b.n, bc = b.c;
-      const uint64_t P0 = t.tlo - kSegB + 4 * tid;
-      if (!FM && ((bn & bc) || (bc & 1))) {  // the bytes' owner tile checks them; here only their planes
-        const bool lead = is_qid_letter(at(P0 - 1));
-        if ((bn & bc) || lead) (void)qid_clean(P0, &bn, &bc, lead, at);
-      }
-      atomic_or_u64(&sh.u.m.d[0], (uint64_t)b.d << (4 * tid));
-      atomic_or_u64(&sh.u.m.n[0], bn << (4 * tid));
-      atomic_or_u64(&sh.u.m.c[0], bc << (4 * tid));
-    }
-  }
+  uint32_t bad = classify_tile<FM>(t, sh, tid, at, true);
   FAST_STAMP(k, 9);
   if (tid < kWave) chunk_list_end(a.cs, a.nchunk, t.tlo, t.thi, cp, sh.c, bk);
   FAST_STAMP(k, 10);
   bk.sync();
+  // a byte outside the grammar ('#' among them) in the tile or in the pre-halo:
+  // blank the comments and classify again (block-uniform, libsvm only)
+  if (!FM && sh.hashy) bad = comments_reclassify(t, sh, bk);
   if (tid == 0) bad |= sh.c.toomany;
   FAST_STAMP(k, 3);
 #if defined(FSVM_ABL_STOP) && FSVM_ABL_STOP == 1  // timing ablation only: stage + classify

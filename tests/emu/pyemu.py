@@ -18,7 +18,13 @@ _BUILT = False
 def build():
     """(Re)build the emulator when its sources changed (make is a no-op otherwise)."""
     global _BUILT
-    subprocess.check_call(["make", "-s", "-C", HERE])
+    import fcntl
+    os.makedirs(os.path.join(HERE, "_build"), exist_ok=True)
+    # pytest-xdist workers share the build dir: one make at a time, so no worker
+    # executes the binary while another is still linking it
+    with open(os.path.join(HERE, "_build", ".lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        subprocess.check_call(["make", "-s", "-C", HERE])
     _BUILT = True
 
 

@@ -107,6 +107,48 @@ def qid_libsvm(rng, nlines, maxfeat=40, violate=False, mixed=False):
     return text.encode("latin-1")
 
 
+def comment_libsvm(rng, nlines, maxfeat=30, long_frac=0.0, violate=False, qid=False, line_comments=False):
+    """libsvm rows with '#' comments where IgnoreCommentAndBlank reads them
+    (libsvm_parser.h:67-83): whole comment lines, a header at the start, and
+    trailing comments after a label, an index, a value or a qid, with or
+    without blanks before the '#'; comment text is any printable byte but a
+    newline (letters, digits, ':', "qid:", more '#').  long_frac: share of
+    comments longer than a tile's pre-halo (64 B).  violate=True adds forms
+    the reference reads otherwise ('#' after a ':' or "qid:", stray letters).
+    line_comments=True adds '#' lines after the first, which the reference
+    does not read as comments (ParseBlock's lines begin at the previous '\\n',
+    which IgnoreCommentAndBlank does not skip: their digits become rows)."""
+    alphabet = "abcdefghijklmnopqrstuvwxyz ABCXYZ0123456789:.+-eE#\t qid:qid !?,;=_/"
+
+    def ctext():
+        n = int(rng.integers(70, 400)) if rng.random() < long_frac else int(rng.integers(0, 50))
+        return "".join(alphabet[int(rng.integers(0, len(alphabet)))] for _ in range(n)).replace("\\t", "\t")
+
+    out = []
+    if rng.random() < 0.5:
+        out.append(rng.choice(["#", " #", "\t# "]) + ctext())
+    for _ in range(nlines):
+        r = rng.random()
+        if line_comments and r < 0.08:
+            out.append(rng.choice(["", " ", "\t"]) + "#" + ctext())
+            continue
+        parts = [_num(rng) if rng.random() < 0.3 else str(int(rng.integers(0, 5)))]
+        if rng.random() < 0.2:
+            parts.append(":" + _num(rng))
+        if qid:
+            parts.append(" qid:" + str(int(rng.integers(0, 1000))))
+        for j in range(int(rng.integers(0, maxfeat + 1))):
+            parts.append(_blank(rng) + _idx(rng) + (":" + _num(rng) if rng.random() < 0.9 else ""))
+        if rng.random() < 0.5:
+            parts.append(rng.choice(["", " ", "  ", "\t", " \t"]) + "#" + ctext())
+        if violate and rng.random() < 0.1:
+            parts.append(rng.choice([" 3:#x", " 3: # y", " qid:#1", " a#", " #:", " 5 :#"]))
+        out.append("".join(parts))
+    seps = ["\n"] * 12 + ["\r\n", "\r"]
+    text = "".join(line + seps[int(rng.integers(0, len(seps)))] for line in out)
+    return text.encode("latin-1")
+
+
 def dense_libsvm(rng, nbytes, style):
     """libsvm text with the shortest runs the grammar allows, so a 16 KiB tile
     holds several thousand runs (the fast kernel's run lists then take

@@ -371,3 +371,44 @@ def test_emu_qid_letter_forms(fmt):
             assert (o["status"] != 0) == failed, (fmt, line, o["msg"], h["error"])
             if not failed:
                 assert diff(h, o) == [], (fmt, line, diff(h, o))
+
+
+def test_emu_fast_comments_vs_oracle():
+    """'#' comments in the single-pass grammar (svm_fast.h comment_erase):
+    comment lines, a header, trailing comments with any text, comments longer
+    than the pre-halo across tile ends, odd chunkings, qid rows; forms the
+    reference reads otherwise go to the exact kernels -- whichever path runs,
+    the reference's result."""
+    rng = np.random.default_rng(5151)
+    paths = {"fast": 0, "exact": 0}
+    for it in range(36):
+        big = it % 3 == 0
+        data = fuzz_text.comment_libsvm(rng, 500 if big else int(rng.integers(1, 30)), 30 if big else 12,
+                                        long_frac=0.0 if it % 2 == 0 else 0.2, violate=it % 4 == 3,
+                                        qid=it % 5 == 2, line_comments=it % 8 == 5)
+        offs = fuzz_text.random_cuts(rng, data, 6, anywhere=it % 3 == 1)
+        kw = {"index_bits": 64} if it % 7 == 1 else {}
+        h = _emu_vs_oracle(data, offs, **kw)
+        paths[h["path"]] += 1
+        if it % 2 == 0 and it % 4 != 3 and it % 3 != 1:  # short comments, no violations, line-aligned cuts
+            assert h["path"] == "fast", (it, data[:300])
+    assert paths["fast"] >= 12 and paths["exact"] >= 3, paths
+
+
+@pytest.mark.parametrize("body", ["x", " 1 2:3 4", "q:i#d"])
+def test_emu_comments_across_tile_ends(body):
+    """A comment whose '#' sits d bytes before a 16 KiB tile end and runs L
+    bytes: inside the next tile's pre-halo (d <= 64) the next tile blanks it
+    itself; further back the tile holding the '#' raises the gate.  Comment
+    text of letters, of digits and ':' (which would parse as features), and
+    of qid letters."""
+    rng = np.random.default_rng(17)
+    base = fuzz_text.uniform_libsvm(rng, 400, 20).replace(b"\r", b"\n")
+    for d in (2, 64, 65, 300):
+        for L in (3, 80, 20000):
+            cut = base.index(b"\n", 16384 - d - 200) + 1  # a line start before the tile end
+            pre = base[:cut] + b"7" + b" " * max(0, 16384 - d - cut - 6) + b" 1:2 "  # '#' right after a pair
+            assert len(pre) == 16384 - d
+            com = (b"#" + (body.encode() * (L // len(body) + 1))[:L]).replace(b"\n", b" ")
+            data = pre + com + b"\n" + base[cut:]
+            _emu_vs_oracle(data, [0, len(data)] if (d + L) % 2 else [0, cut, len(data)])

@@ -304,6 +304,69 @@ def test_gpu_fast_qid_vs_oracle(dm):
     assert paths["fast"] >= 60 and paths["exact"] >= 20, paths
 
 
+def test_gpu_fast_comments_vs_oracle(dm):
+    """'#' comments through the single-pass kernel (svm_fast.h comment_erase):
+    headers, trailing comments with any text, comments longer than the
+    pre-halo, qid rows; '#' lines after the first and the forms the reference
+    reads otherwise take the exact path -- both equal the oracle."""
+    rng = np.random.default_rng(6161)
+    paths = {"fast": 0, "exact": 0}
+    for it in range(120):
+        big = it % 10 == 0
+        data = fuzz_text.comment_libsvm(rng, 3000 if big else int(rng.integers(1, 40)), 60 if big else 16,
+                                        long_frac=0.0 if it % 2 == 0 else 0.2, violate=it % 4 == 3,
+                                        qid=it % 5 == 2, line_comments=it % 8 == 5)
+        offs = fuzz_text.random_cuts(rng, data, int(rng.integers(0, 8)), anywhere=it % 3 == 1)
+        kw = {"index_bits": 64} if it % 7 == 1 else {}
+        h = _gpu_vs_oracle_paths(dm, data, offs, **kw)
+        paths[h["path"]] += 1
+        if it % 2 == 0 and it % 4 != 3 and it % 3 != 1 and not big:
+            assert h["path"] == "fast", it
+    assert paths["fast"] >= 30 and paths["exact"] >= 10, paths
+
+
+@pytest.mark.parametrize("body", ["x", " 1 2:3 4", "q:i#d"])
+def test_gpu_comments_across_tile_ends(dm, body):
+    """A comment d bytes before a 16 KiB tile end, L bytes long: the next tile
+    blanks it from its pre-halo when the '#' and the pair before it lie there,
+    else the gate hands over."""
+    rng = np.random.default_rng(17)
+    base = fuzz_text.uniform_libsvm(rng, 400, 20).replace(b"\r", b"\n")
+    for d in (1, 2, 40, 63, 64, 65, 300):
+        for L in (0, 3, 80, 600, 20000):
+            cut = base.index(b"\n", 16384 - d - 200) + 1
+            pre = base[:cut] + b"7" + b" " * max(0, 16384 - d - cut - 6) + b" 1:2 "  # '#' right after a pair
+            com = (b"#" + (body.encode() * (L // len(body) + 1))[:L]).replace(b"\n", b" ")
+            data = pre + com + b"\n" + base[cut:]
+            for offs in ([0, len(data)], [0, cut, len(data)]):
+                h = _gpu_vs_oracle_paths(dm, data, offs)
+                if d <= 60 and L <= 600 and len(offs) == 2:  # the pair before the '#' in the pre-halo
+                    assert h["path"] == "fast", (d, L)
+
+
+def test_gpu_comment_bench_size_fast_equals_exact(dm):
+    """Config 2 rows, each with a trailing '# row <r>' comment, and a header
+    line: single-pass == exact bit for bit (the comment path in every tile)."""
+    import torch
+    text, _ = synth.rows(synth.LIBSVM, 1 << 18, 128, seed=3)
+    body = bytes(text).replace(b"\n", b" # c:1 qid:2 #x\n")
+    data = b"# header: label idx:val ...\n" + body
+    arr = np.frombuffer(data, dtype=np.uint8)
+    starts = dm.text_chunk_starts(arr)
+    d_text, d_cs = torch.from_numpy(arr.copy()).cuda(), torch.from_numpy(starts).cuda()
+    outs = {}
+    for exact in (False, True):
+        p = dm.DeviceParser("libsvm", flags=dm.FLAG_EXACT if exact else 0)
+        out = p.parse(d_text, d_cs)
+        assert out["error"] == 0 and out["path"] == (1 if exact else 0), (exact, out["path"])
+        outs[exact] = out
+    assert outs[False]["counts"][:7] == outs[True]["counts"][:7]
+    for k in ("offset", "label", "index", "value"):
+        a, b = outs[False][k], outs[True][k]
+        assert torch.equal(a.view(torch.int32) if a.dtype == torch.float32 else a,
+                           b.view(torch.int32) if b.dtype == torch.float32 else b), k
+
+
 def test_gpu_qid_bench_size_fast_equals_exact(dm):
     """The qid bench config (1M rows x 128 nnz, qid:<row/16> on every row):
     single-pass == exact bit for bit, qid[r] = r / 16."""
