@@ -40,6 +40,7 @@ CONFIGS = {
     "libsvm_32m_x64": ("libsvm", 32 << 20, 64, 4),
     "libfm_1m_x64": ("libfm", 1 << 20, 64, None),  # SURVEY 8(f) row 3, not a BASELINE config
     "libsvm_qid_1m_x128": ("libsvm_qid", 1 << 20, 128, None),  # config 2's rows with qid: (ranking data)
+    "libsvm_cmt_1m_x128": ("libsvm_cmt", 1 << 20, 128, None),  # config 2's rows with '#' comments
 }
 DESC = {
     "libsvm_1m_x128": "libsvm 1M rows x 128 nnz/row, device-resident",
@@ -48,11 +49,14 @@ DESC = {
     "libsvm_32m_x64": "libsvm 32M rows x 64 nnz/row, chunks sharded across GPUs",
     "libfm_1m_x64": "libfm 1M rows x 64 field:id:value/row, device-resident",
     "libsvm_qid_1m_x128": "libsvm 1M rows x 128 nnz/row with qid:<row/16> on every row, device-resident",
+    "libsvm_cmt_1m_x128": "libsvm 1M rows x 128 nnz/row, a '# row <r>' comment on every row and a header, device-resident",
 }
-SYNTH = {"libsvm": synth.LIBSVM, "csv": synth.CSV, "libfm": synth.LIBFM, "libsvm_qid": synth.LIBSVM_QID}
+SYNTH = {"libsvm": synth.LIBSVM, "csv": synth.CSV, "libfm": synth.LIBFM, "libsvm_qid": synth.LIBSVM_QID,
+         "libsvm_cmt": synth.LIBSVM_CMT}
 # the arithmetic the path computes in (values decoded to f32 through the
 # reference's f64 fraction divide; indices / fields as u32)
 DTYPE = {"libsvm": "f32 values / u32 index", "libsvm_qid": "f32 values / u32 index / u64 qid",
+         "libsvm_cmt": "f32 values / u32 index",
          "csv": "f32 values", "libfm": "f32 values / u32 index / u32 field"}
 
 
@@ -166,7 +170,7 @@ def main():
     d_starts = torch.from_numpy(starts).to(dev)
     nbytes = int(text.size)
     pkw = {"label_column": args.label_column} if fmt == "csv" else {}
-    pfmt = "libsvm" if fmt == "libsvm_qid" else fmt
+    pfmt = "libsvm" if fmt in ("libsvm_qid", "libsvm_cmt") else fmt
     p = dmlc_amd.DeviceParser(pfmt, tile_bytes=args.tile_bytes, **pkw)
     res = torch.zeros(16, dtype=torch.int64, device=dev)
     counts = p.count(d_text, d_starts, result=res)

@@ -289,31 +289,59 @@ DA_HD bool carry_fast(uint64_t d1, uint64_t n1r, uint64_t c1r, uint32_t *dc, uin
 // line's '\n' (libsvm_parser.h:91-96), which IgnoreCommentAndBlank does not
 // skip, so there ParsePair reads the '#' line's digits as the label and the
 // exact kernels take it.
-struct CmtBlock {
-  uint64_t A, B;  // comment-opening '#', comment ends
-  uint32_t rout;  // the byte after the block is reachable
-  uint32_t free_;  // all blanks, no range start: rout = the block's reach-in
+// Byte masks of 64 staged bytes (16-byte aligned), four bytes per SWAR step.
+struct CmtMasks {
+  uint64_t h, nl, bl, dg;  // '#', newline, blank, digitchar
 };
-// the 64 staged bytes at p; S: range starts among them; r: reach-in
-DA_HD CmtBlock comment_block(const uint8_t *p, uint64_t S, uint32_t r) {
-  uint64_t h = 0, nl = 0, bl = 0, dg = 0;
-#pragma unroll 4
-  for (int i = 0; i < 64; ++i) {
-    const uint32_t b = p[i];
-    h |= (uint64_t)(b == '#') << i;
-    nl |= (uint64_t)is_nl(b) << i;
-    bl |= (uint64_t)is_blank(b) << i;
-    dg |= (uint64_t)is_digitchar(b) << i;
+DA_HD uint32_t swar_zero_hi(uint32_t t) {  // 0x80 in each zero byte of t
+  return ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u;
+}
+DA_HD uint32_t hi_nib(uint32_t m) { return (m * 0x00204081u) >> 28; }  // byte high bits -> 4 bits
+DA_HD CmtMasks comment_masks(const uint8_t *p) {
+  CmtMasks k{0, 0, 0, 0};
+#pragma unroll 1
+  for (int q = 0; q < 4; ++q) {
+    uint32_t w[4];
+    load16(p + 16 * q, w);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t x = w[j];
+      const uint32_t lo = (x | 0x80808080u) - 0x30303030u, hi = (x | 0x80808080u) - 0x3A3A3A3Au;
+      const uint32_t dig = lo & ~hi & ~x & 0x80808080u;
+      const uint32_t dc = dig | swar_zero_hi(x ^ 0x2B2B2B2Bu) | swar_zero_hi(x ^ 0x2D2D2D2Du) |
+                          swar_zero_hi(x ^ 0x2E2E2E2Eu) | swar_zero_hi((x | 0x20202020u) ^ 0x65656565u);
+      const uint32_t nl = swar_zero_hi(x ^ 0x0A0A0A0Au) | swar_zero_hi(x ^ 0x0D0D0D0Du);
+      const uint32_t bl = swar_zero_hi(x ^ 0x20202020u) | swar_zero_hi(x ^ 0x09090909u);
+      const int sh = 16 * q + 4 * j;
+      k.h |= (uint64_t)hi_nib(swar_zero_hi(x ^ 0x23232323u)) << sh;
+      k.nl |= (uint64_t)hi_nib(nl) << sh;
+      k.bl |= (uint64_t)hi_nib(bl) << sh;
+      k.dg |= (uint64_t)hi_nib(dc) << sh;
+    }
   }
-  const uint64_t ok = (dg << 1) | S, seeds = ok & bl;
+  return k;
+}
+// "Reachable" bytes of a block with reach-in r: after a digitchar or at a
+// range start (S), through blanks.  *rout: the byte after the block is.
+DA_HD uint64_t reach_of(const CmtMasks &k, uint64_t S, uint32_t r, uint32_t *rout) {
+  const uint64_t ok = (k.dg << 1) | S, seeds = ok & k.bl;
   uint32_t ro;
-  const uint64_t reach = ok | (add_carry(bl, seeds, r, &ro) ^ bl ^ seeds);
-  CmtBlock o;
-  o.A = h & reach;
-  o.B = nl | (S & ~o.A);  // a range start ends a comment, unless it opens one
-  o.rout = ro | (uint32_t)(dg >> 63);
-  o.free_ = (~bl == 0) && S == 0;
-  return o;
+  const uint64_t reach = ok | (add_carry(k.bl, seeds, r, &ro) ^ k.bl ^ seeds);
+  *rout = ro | (uint32_t)(k.dg >> 63);
+  return reach;
+}
+// reach-out as a function of reach-in (bit 0 = f(0), bit 1 = f(1))
+DA_HD uint32_t reach_fn(const CmtMasks &k, uint64_t S) {
+  uint32_t r0, r1;
+  (void)reach_of(k, S, 0u, &r0);
+  (void)reach_of(k, S, 1u, &r1);
+  return r0 | (r1 << 1);
+}
+// comment-opening '#' (A) and comment ends (B) of a block with reach-in r
+DA_HD void comment_ab(const CmtMasks &k, uint64_t S, uint32_t r, uint64_t *A, uint64_t *B) {
+  uint32_t ro;
+  *A = k.h & reach_of(k, S, r, &ro);
+  *B = k.nl | (S & ~*A);  // a range start ends a comment, unless it opens one
 }
 // open-after as a function of open-before: bit 0 = f(0), bit 1 = f(1)
 DA_HD uint32_t comment_fn(uint64_t A, uint64_t B) {
@@ -351,58 +379,64 @@ DA_HD uint64_t cs_bits(const TileCommon &c, uint64_t lo) {
 // threads.  Returns 1 (gate) when the tile after this one cannot see from its
 // pre-halo that a comment is open at its start.
 template <class BK>
-DA_HDF uint32_t comment_erase(uint64_t tlo, uint64_t thi, uint64_t n, TileCommon &c, BK &bk) {
+DA_HDF uint32_t comment_erase(uint64_t tlo, uint64_t thi, uint64_t n, TileCommon &c, uint32_t *note, BK &bk) {
   const int tid = bk.tid();
   uint8_t *txt = c.text;
-  auto block_at = [&](int j, uint32_t r) {  // segment j of the tile, -1 the pre-halo
-    return comment_block(txt + kPre + j * kSegB, cs_bits(c, tlo + (int64_t)j * kSegB), r);
-  };
-  // the tile start: a comment open at the end of the pre-halo, the pre-halo
-  // read on its own (reach-in 0), as the tile before checks it
-  CmtBlock h{0, 0, 0, 0};
-  uint32_t c0 = 0;
-  if (tlo > 0) {
-    h = block_at(-1, 0u);
-    c0 = comment_fn(h.A, h.B) & 1u;
-  }
-  // reach-in: back over the staged bytes to the first block that decides it
-  uint32_t r = 0;
-  for (int j = tid - 1; j >= (tlo > 0 ? -1 : 0); --j) {
-    const CmtBlock b = block_at(j, 0u);
-    if (!b.free_ || j == -1) {
-      r = b.rout;
-      break;
-    }
-  }
   const uint64_t P = tlo + (uint64_t)tid * kSegB;
-  const CmtBlock m = block_at(tid, r);
-  const uint32_t f = comment_fn(m.A, m.B);
-  // the next tile reads the state at its start from its pre-halo (this
-  // segment) alone, reach-in 0
-  uint32_t f_next = 0;
-  if (tid == kThreads - 1) {
-    const CmtBlock nx = block_at(tid, 0u);
-    f_next = comment_fn(nx.A, nx.B) & 1u;
+  const CmtMasks k = comment_masks(txt + kPre + tid * kSegB);
+  const uint64_t S = cs_bits(c, P);
+  // the pre-halo read on its own (reach-in 0, no comment open before it): the
+  // tile start's reach and comment state, as the tile before checks them
+  uint64_t hA = 0, hB = 0;
+  if (tid == 0 && tlo > 0) {
+    const CmtMasks kh = comment_masks(txt);
+    const uint64_t Sh = cs_bits(c, tlo - kPre);
+    uint32_t r0;
+    (void)reach_of(kh, Sh, 0u, &r0);
+    comment_ab(kh, Sh, 0u, &hA, &hB);
+    const uint32_t c0 = comment_fn(hA, hB) & 1u;
+    *note = 1u | (r0 << 1) | (c0 << 2);  // (stays nonzero: the caller's branch read it)
   }
   uint32_t tot;
-  const uint32_t pre = bk.exclusive(f, 2u, CommentFnCompose(), &tot);  // (its barriers order the reads above)
-  const uint32_t cin = (pre >> c0) & 1u;
+  const uint32_t rpre = bk.exclusive(reach_fn(k, S), 2u, CommentFnCompose(), &tot);
+  const uint32_t r = (rpre >> ((*note >> 1) & 1u)) & 1u;
+  uint64_t A, B;
+  comment_ab(k, S, r, &A, &B);
+  const uint32_t f = comment_fn(A, B);
+  uint32_t f_next = 0;  // the next tile's reading of its pre-halo (this segment)
+  if (tid == kThreads - 1) {
+    uint64_t An, Bn;
+    comment_ab(k, S, 0u, &An, &Bn);
+    f_next = comment_fn(An, Bn) & 1u;
+  }
+  const uint32_t pre = bk.exclusive(f, 2u, CommentFnCompose(), &tot);
+  const uint32_t cin = (pre >> ((*note >> 2) & 1u)) & 1u;
   uint32_t co, gate = 0;
-  blank_bytes(txt + kPre + tid * kSegB, comment_mask(m.A, m.B, cin, &co));
+  const uint64_t M = comment_mask(A, B, cin, &co);
+  blank_bytes(txt + kPre + tid * kSegB, M);
+  uint32_t changed = M != 0;  // bit 0: my segment, bit 1: the pre-halo, bit 2: the post-halo
   if (tid == 0 && tlo > 0) {
     uint32_t ch;
-    blank_bytes(txt, comment_mask(h.A, h.B, 0u, &ch));
+    const uint64_t Mh = comment_mask(hA, hB, 0u, &ch);
+    blank_bytes(txt, Mh);
+    if (Mh) changed |= 2u;
   }
   if (tid == kThreads - 1) {
     if (thi < n && P + kSegB == thi && !(cs_bits(c, thi) & 1u) && co != f_next) gate = 1;
-    uint32_t ci = co, ri = m.rout;
+    uint32_t ci = co, ri;
+    (void)reach_of(k, S, r, &ri);
     for (int s = 0; s < kPost / kSegB; ++s) {
-      const CmtBlock b = block_at(kThreads + s, ri);
-      blank_bytes(txt + kPre + kTile + s * kSegB, comment_mask(b.A, b.B, ci, &ci));
-      ri = b.rout;
+      const CmtMasks kp = comment_masks(txt + kPre + kTile + s * kSegB);
+      const uint64_t Sp = cs_bits(c, tlo + kTile + (uint64_t)s * kSegB);
+      uint64_t Ap, Bp;
+      comment_ab(kp, Sp, ri, &Ap, &Bp);
+      (void)reach_of(kp, Sp, ri, &ri);
+      const uint64_t Mp = comment_mask(Ap, Bp, ci, &ci);
+      blank_bytes(txt + kPre + kTile + s * kSegB, Mp);
+      if (Mp) changed |= 4u;
     }
   }
-  return gate;
+  return gate | (changed << 1);
 }
 
 // Runs, roles and counts of segment tid (positions P .. P+63).
@@ -703,20 +737,28 @@ FSVM_COLD bool slow_uint(const uint8_t *text, uint64_t q, uint64_t lim, int wide
   return parse_uint(src, q, wide != 0, v);
 }
 
-// Classification of segment tid (and, lanes 0..15, of the pre-halo): the LDS
-// planes, the digit-plane words; returns the segment's grammar flag.  `first`:
-// pass 0, which also notes bytes outside the grammar (sh.hashy).
+// Classification of segment tid (parts bit 0), of the pre-halo (bit 1: lanes
+// 0..15, OR-ed into slot 0) and of the 16 bytes after the tile (bit 2: lane
+// kWave): the LDS planes and digit-plane words; returns the segment's grammar
+// flag.  `first`: pass 0, which also notes bytes outside the grammar.
 template <bool FM, class At>
-DA_HDF uint32_t classify_tile(const Tile &t, Shared &sh, int tid, At at, bool first) {
+DA_HDF uint32_t classify_tile(const Tile &t, Shared &sh, int tid, At at, bool first, uint32_t parts) {
   uint32_t bad = 0;
-  Masks m = classify64_lut(sh.c.text + kPre + tid * kSegB, sh.cls);
-  const uint64_t P0 = t.tlo + (uint64_t)tid * kSegB;
-  if ((m.n & m.c) || ((m.c & 1) && P0 > 0 && is_qid_letter(at(P0 - 1)))) {  // letters: "qid:" tokens
-    if (FM || !qid_clean(P0, &m.n, &m.c, P0 > 0 && is_qid_letter(at(P0 - 1)), at)) bad = 1;
+  if (parts & 1u) {
+    Masks m = classify64_lut(sh.c.text + kPre + tid * kSegB, sh.cls);
+    const uint64_t P0 = t.tlo + (uint64_t)tid * kSegB;
+    if ((m.n & m.c) || ((m.c & 1) && P0 > 0 && is_qid_letter(at(P0 - 1)))) {  // letters: "qid:" tokens
+      if (FM || !qid_clean(P0, &m.n, &m.c, P0 > 0 && is_qid_letter(at(P0 - 1)), at)) bad = 1;
+    }
+    sh.gw[2 * tid] = (uint32_t)m.g;
+    sh.gw[2 * tid + 1] = (uint32_t)(m.g >> 32);
+    sh.u.m.d[tid + 1] = m.d;
+    sh.u.m.n[tid + 1] = m.n;
+    sh.u.m.c[tid + 1] = m.c;
+    bad |= m.bad;
+    if (!FM && first && m.bad) sh.hashy = 1;
   }
-  sh.gw[2 * tid] = (uint32_t)m.g;
-  sh.gw[2 * tid + 1] = (uint32_t)(m.g >> 32);
-  if (tid == kWave) {  // digits of the 16 bytes after the tile (windows of my last runs)
+  if ((parts & 4u) && tid == kWave) {  // digits of the 16 bytes after the tile (windows of my last runs)
     uint32_t g = 0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -726,12 +768,7 @@ DA_HDF uint32_t classify_tile(const Tile &t, Shared &sh, int tid, At at, bool fi
     }
     sh.gw[2 * kThreads] = g;
   }
-  sh.u.m.d[tid + 1] = m.d;
-  sh.u.m.n[tid + 1] = m.n;
-  sh.u.m.c[tid + 1] = m.c;
-  bad |= m.bad;
-  if (!FM && first && m.bad) sh.hashy = 1;
-  if (tid < 16 && t.tlo > 0) {
+  if ((parts & 2u) && tid < 16 && t.tlo > 0) {
     uint32_t x;
     memcpy(&x, sh.c.text + (kPre - kSegB) + 4 * tid, 4);
     const Nib b = classify_dword_lut(x, sh.cls);
@@ -749,22 +786,25 @@ DA_HDF uint32_t classify_tile(const Tile &t, Shared &sh, int tid, At at, bool fi
   return bad;
 }
 
-// Pass 1 (libsvm): blank the comments, classify again; all threads, after the
-// chunk list is known.  Returns the segment's grammar flag.
+// Pass 1 (libsvm): blank the comments and classify again what changed; all
+// threads, after the chunk list is known.  bad0: the segment's pass-0 flag.
 template <class BK>
-DA_HDF uint32_t comments_reclassify(const Tile t, Shared &sh, BK &bk) {
+DA_HDF uint32_t comments_reclassify(const Tile t, Shared &sh, uint32_t bad0, BK &bk) {
   const int tid = bk.tid();
   const FastSvmArgs &a = *t.a;
-  const uint32_t cgate = comment_erase(t.tlo, t.thi, a.n, sh.c, bk);
-  if (tid == 0) sh.u.m.d[0] = sh.u.m.n[0] = sh.u.m.c[0] = 0;
+  const uint32_t e = comment_erase(t.tlo, t.thi, a.n, sh.c, &sh.hashy, bk);
+  if (e & 12u) atomic_or_u32(&sh.hashy, (e & 12u) << 1);  // pre-halo / post-halo blanked: note bits 3 / 4
+  if (tid == 0 && (e & 4u)) sh.u.m.d[0] = sh.u.m.n[0] = sh.u.m.c[0] = 0;
   bk.sync();
   auto at = [&](uint64_t p) -> uint32_t {
     if (p >= a.n) return 0u;
     return p + kPre >= t.tlo ? (uint32_t)sh.c.text[p - t.tlo + kPre] : (uint32_t)a.text[p];
   };
-  const uint32_t bad = classify_tile<false>(t, sh, tid, at, false);
+  const uint32_t note = sh.hashy;
+  const uint32_t parts = ((e >> 1) & 1u) | ((note >> 2) & 6u);
+  const uint32_t bad = classify_tile<false>(t, sh, tid, at, false, parts);
   bk.sync();
-  return bad | cgate;
+  return ((e >> 1) & 1u ? bad : bad0) | (e & 1u);
 }
 
 // MODE 1: count only (size query); MODE 2: parse and write.
@@ -813,14 +853,14 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
     if (p >= a.n) return 0u;
     return p + kPre >= t.tlo ? (uint32_t)sh.c.text[p - t.tlo + kPre] : (uint32_t)a.text[p];
   };
-  uint32_t bad = classify_tile<FM>(t, sh, tid, at, true);
+  uint32_t bad = classify_tile<FM>(t, sh, tid, at, true, 7u);
   FAST_STAMP(k, 9);
   if (tid < kWave) chunk_list_end(a.cs, a.nchunk, t.tlo, t.thi, cp, sh.c, bk);
   FAST_STAMP(k, 10);
   bk.sync();
   // a byte outside the grammar ('#' among them) in the tile or in the pre-halo:
   // blank the comments and classify again (block-uniform, libsvm only)
-  if (!FM && sh.hashy) bad = comments_reclassify(t, sh, bk);
+  if (!FM && sh.hashy) bad = comments_reclassify(t, sh, bad, bk);
   if (tid == 0) bad |= sh.c.toomany;
   FAST_STAMP(k, 3);
 #if defined(FSVM_ABL_STOP) && FSVM_ABL_STOP == 1  // timing ablation only: stage + classify

@@ -14,6 +14,8 @@
  *    values with a field in [0,32) per feature (libfm_parser.h:67-144).
  *  libsvm+qid row (fmt 3): "<label> qid:<q>( <id>:<value>)*\n", the libsvm
  *    row with q = row / 16 (ranking data, libsvm_parser.h:119-132).
+ *  libsvm+comment row (fmt 4): the libsvm row with a trailing comment
+ *    " # row <r>" (libsvm_parser.h:67-83), and a '#' header line first.
  */
 #include <stdint.h>
 #include <stdio.h>
@@ -32,7 +34,7 @@ static inline uint64_t row_state(uint64_t seed, uint64_t r) {
   return s;
 }
 
-static size_t fmt_libsvm_row(char *o, uint64_t seed, uint64_t r, int K, int qid) {
+static size_t fmt_libsvm_row(char *o, uint64_t seed, uint64_t r, int K, int qid, int cmt) {
   uint64_t s = row_state(seed, r);
   char *p = o;
   *p++ = (char)('0' + (sm64(&s) & 1));
@@ -45,6 +47,7 @@ static size_t fmt_libsvm_row(char *o, uint64_t seed, uint64_t r, int K, int qid)
     float v = (float)(x >> 40) * (1.0f / 16777216.0f);
     p += sprintf(p, " %llu:%.9g", (unsigned long long)id, (double)v);
   }
+  if (cmt) p += sprintf(p, " # row %llu", (unsigned long long)r);
   *p++ = '\n';
   return (size_t)(p - o);
 }
@@ -79,7 +82,7 @@ static size_t fmt_csv_row(char *o, uint64_t seed, uint64_t r, int C) {
 
 /* upper bound on the bytes of `nrows` rows */
 size_t synth_bound(int fmt, uint64_t nrows, int width) {
-  return fmt == 0 || fmt == 3 ? nrows * (size_t)(2 + 26 + width * 26)
+  return fmt == 0 || fmt == 3 || fmt == 4 ? nrows * (size_t)(2 + 28 + width * 26) + 32
                   : fmt == 2 ? nrows * (size_t)(2 + width * 30) : nrows * (size_t)(width * 18 + 2);
 }
 
@@ -101,7 +104,8 @@ size_t synth_rows(int fmt, uint64_t row0, uint64_t nrows, int width, uint64_t se
     size_t n = 0;
     for (uint64_t r = r0; r < r1; ++r) {
       if (line_off) line_off[r] = n; /* block-relative; fixed below */
-      n += fmt == 0 || fmt == 3 ? fmt_libsvm_row(buf + n, seed, row0 + r, width, fmt == 3)
+      if (fmt == 4 && row0 + r == 0) n += (size_t)sprintf(buf + n, "# label id:value ... # row r\n");
+      n += fmt == 0 || fmt == 3 || fmt == 4 ? fmt_libsvm_row(buf + n, seed, row0 + r, width, fmt == 3, fmt == 4)
                     : fmt == 2 ? fmt_libfm_row(buf + n, seed, row0 + r, width)
                                : fmt_csv_row(buf + n, seed, row0 + r, width);
     }
