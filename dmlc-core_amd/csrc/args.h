@@ -87,10 +87,12 @@ struct FastCsvArgs {
   uint32_t delim;
   int skip_if_gated;
   int label_col;        // CSVParserParam::label_column, -1 = none
+  int weight_col;       // CSVParserParam::weight_column, -1 = none (csv_fast_columns_ok)
   uint64_t *offset;
   float *label;         // one per row when label_col >= 0
-  uint64_t *labsum;     // [kLabShards][8], zeroed per launch: words 0/1 = sum(labels - rows),
-                        // sum(first delimiters - rows), sharded by tile (csv_fast.h)
+  float *weight;        // one per row when weight_col >= 0
+  uint64_t *labsum;     // [kLabShards][8], zeroed per launch: words 0/1/2 = sum(labels - rows),
+                        // sum(first delimiters - rows), sum(weights - rows), sharded by tile (csv_fast.h)
   void *index;
   float *value;
   uint64_t cap[8];
@@ -100,6 +102,18 @@ struct FastCsvArgs {
   unsigned long long *err;
   uint64_t *res;
 };
+
+// Label / weight columns the single-pass CSV kernel takes: every row holds a
+// non-empty field at each (checked on the device), and then a row always keeps
+// a non-special field -- unless the special columns are {0} or {0, 1}, where a
+// row of only those fields is the reference's fatal "Delimiter not found"
+// (csv_parser.h:128-132): label column 0 alone is checked on the device, the
+// weight forms go to the exact kernels.
+DA_HD bool csv_fast_columns_ok(int label_col, int weight_col) {
+  if (weight_col < 0) return true;
+  if (weight_col == label_col || weight_col == 0) return false;
+  return label_col < 0 || (label_col > weight_col ? label_col : weight_col) >= 2;
+}
 
 struct CsvArgs {
   const uint8_t *text;

@@ -283,7 +283,9 @@ int dmlc_amd_parse(const void *d_text, uint64_t nbytes, const uint64_t *d_chunk_
     f.delim = a.delim;
     f.skip_if_gated = phase == dmlc_amd::kPhaseFill;
     f.label_col = prm->label_column;
+    f.weight_col = prm->weight_column;
     f.label = reinterpret_cast<float *>(out->label);
+    f.weight = out->weight;
     f.labsum = labsum;
     f.offset = a.offset;
     f.index = a.index;
@@ -294,9 +296,10 @@ int dmlc_amd_parse(const void *d_text, uint64_t nbytes, const uint64_t *d_chunk_
     f.gate = ctl;
     f.err = ferr;
     f.res = res;
-    // the uniform-grammar CSV kernel: float values, no weight column, a
-    // delimiter the number decoder cannot consume (csv_fast.h)
-    const bool use_fast = nbytes > 0 && prm->value_type == DMLC_AMD_F32 && prm->weight_column < 0 &&
+    // the uniform-grammar CSV kernel: float values, label / weight columns it
+    // takes, a delimiter the number decoder cannot consume (csv_fast.h)
+    const bool use_fast = nbytes > 0 && prm->value_type == DMLC_AMD_F32 &&
+                          dmlc_amd::csv_fast_columns_ok(prm->label_column, prm->weight_column) &&
                           a.fast_delim && !(prm->flags & DMLC_AMD_FLAG_EXACT);
     e = dmlc_amd::launch_csv(a, f, use_fast, res, phase, s);
   } else {  // DMLC_AMD_LIBFM

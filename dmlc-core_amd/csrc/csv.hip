@@ -25,7 +25,15 @@ __global__ void __launch_bounds__(kThreads, FCSV_MINW) csv_fast_tile(FastCsvArgs
   __shared__ __attribute__((aligned(16))) fcsv::Shared sh;
   __shared__ uint64_t scratch[kBlockScratchU64];
   DevBlock bk{scratch};
-  fcsv::tile<MODE>(a, sh, bk, blockIdx.x);
+  fcsv::tile<MODE, false>(a, sh, bk, blockIdx.x);
+}
+// with a label and / or weight column
+template <int MODE>
+__global__ void __launch_bounds__(kThreads, FCSV_MINW) csv_fast_tile_sp(FastCsvArgs a) {
+  __shared__ __attribute__((aligned(16))) fcsv::Shared sh;
+  __shared__ uint64_t scratch[kBlockScratchU64];
+  DevBlock bk{scratch};
+  fcsv::tile<MODE, true>(a, sh, bk, blockIdx.x);
 }
 
 // fill phase after a count phase that fell back to the exact kernels: reopen
@@ -42,13 +50,13 @@ __global__ void reopen_kernel(uint64_t *res, uint64_t *offset, uint64_t cap_rows
 // input to the exact kernels
 __global__ void label_check_kernel(const uint64_t *labsum, uint32_t *gate) {
   const uint32_t i = threadIdx.x;  // kLabShards threads, one wave
-  const uint64_t s0 = labsum[i * 8], s1 = labsum[i * 8 + 1];
-  uint64_t a = s0, b = s1;
+  uint64_t a = labsum[i * 8], b = labsum[i * 8 + 1], c = labsum[i * 8 + 2];
   for (int d = 32; d >= 1; d >>= 1) {
     a += __shfl_xor(a, d, kWave);
     b += __shfl_xor(b, d, kWave);
+    c += __shfl_xor(c, d, kWave);
   }
-  if (i == 0 && (a != 0 || b != 0)) *gate |= 1u;
+  if (i == 0 && (a != 0 || b != 0 || c != 0)) *gate |= 1u;
 }
 
 // the error of whichever path produced the result
@@ -77,19 +85,22 @@ hipError_t launch_csv(const CsvArgs &a, const FastCsvArgs &f, bool use_fast, uin
   if (use_fast) {
     if ((e = hipMemsetAsync(f.err, 0xFF, sizeof(uint64_t), s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(f.lb, 0, (size_t)f.ntiles * 8 * sizeof(uint64_t), s)) != hipSuccess) return e;
-    if (f.label_col >= 0 &&
+    if ((f.label_col >= 0 || f.weight_col >= 0) &&
         (e = hipMemsetAsync(f.labsum, 0, kLabShards * 8 * sizeof(uint64_t), s)) != hipSuccess)
       return e;
+    const bool sp = f.label_col >= 0 || f.weight_col >= 0;
     if (phase == kPhaseCount) {
       prof_mark(0, s, "csv_fast_tile<1>");
-      csv_fast_tile<1><<<f.ntiles, kThreads, 0, s>>>(f);
+      if (sp) csv_fast_tile_sp<1><<<f.ntiles, kThreads, 0, s>>>(f);
+      else csv_fast_tile<1><<<f.ntiles, kThreads, 0, s>>>(f);
       prof_mark(1, s, "csv_fast_tile<1>");
     } else {
       prof_mark(0, s, "csv_fast_tile<2>");
-      csv_fast_tile<2><<<f.ntiles, kThreads, 0, s>>>(f);
+      if (sp) csv_fast_tile_sp<2><<<f.ntiles, kThreads, 0, s>>>(f);
+      else csv_fast_tile<2><<<f.ntiles, kThreads, 0, s>>>(f);
       prof_mark(1, s, "csv_fast_tile<2>");
     }
-    if (f.label_col >= 0) label_check_kernel<<<1, kLabShards, 0, s>>>(f.labsum, gate);
+    if (f.label_col >= 0 || f.weight_col >= 0) label_check_kernel<<<1, kLabShards, 0, s>>>(f.labsum, gate);
   } else if ((e = hipMemsetAsync(f.err, 0xFF, sizeof(uint64_t), s)) != hipSuccess) {
     return e;
   }

@@ -54,7 +54,9 @@ struct Shared {  // LDS of one workgroup
   DecTables dt;
   uint32_t gw[2 * kThreads + 2];  // digit plane as words: 2t, 2t+1 segment t; 2 kThreads: the post-halo
   uint64_t segc;      // the tile's segmented carry (delimiters since the last row start before it)
-  uint32_t nlab, nfirst;  // label_col >= 0: label tokens / first delimiters of rows in this tile
+  uint32_t nlab, nfirst;  // label tokens (bits 0-15) and weight tokens (16-31) / first delimiters
+                          // of rows in this tile (a tile holds < 2^16 tokens; one word keeps the
+                          // LDS footprint -- 16 more bytes cost the plain kernel 8%)
   uint32_t pend[kTile / kPassTokens + 2];  // token counts at the end of each pass
   uint32_t npass;
 };
@@ -161,7 +163,9 @@ struct Tile {
 };
 
 // MODE 1: count only (size query); MODE 2: parse and write.
-template <int MODE, class BK>
+// SP: label / weight columns may be set (a separate kernel, so the plain
+// form carries none of their code)
+template <int MODE, bool SP, class BK>
 DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
   // Tile k = workgroup k (its blockIdx).  The look-back needs every tile's
   // predecessors to become resident eventually; workgroups are dispatched in
@@ -295,7 +299,9 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
   constexpr int kB = FCSV_KB;  // tokens decoded before the look-back
   float vb[kB > 0 ? kB : 1];
   uint64_t mT = T;
-  const bool has_lab = a.label_col >= 0;
+  const bool has_lab = SP && a.label_col >= 0, has_w = SP && a.weight_col >= 0;
+  const bool has_sp = has_lab || has_w;  // special columns: tokens stored per token, not listed
+  const uint64_t nsp = (has_lab ? 1u : 0u) + (has_w ? 1u : 0u);
   // Without a label column the tokens go to an LDS list in output order
   // (svm_fast.h's run lists): each wave decodes ceil(tokens / 256) values per
   // thread and consecutive lanes store consecutive values and column ids.  The
@@ -321,7 +327,7 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
     }
     (void)e0;
   };
-  if (MODE == 2 && !has_lab) {
+  if (MODE == 2 && !has_sp) {
     if (nT > kPassTokens) {  // block-uniform: several passes
       const uint32_t own = (uint32_t)popc64(T);
       mypass = exT / kPassTokens;
@@ -366,6 +372,7 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
   // csv_parser.h:128-132), (first delimiters - rows) into labsum; a nonzero
   // sum sets the gate after this kernel and the exact kernels redo the input.
   const uint64_t Lc = has_lab ? (uint64_t)a.label_col : ~0ull;
+  const uint64_t Wc = has_w ? (uint64_t)a.weight_col : ~0ull;  // weight_column likewise (:113-114)
   const uint64_t eR = bRows + (ex & 0xFFFF), eT = bVal + ((ex >> 16) & 0xFFFF);
   const uint64_t sex = ex >> 32;  // segmented exclusive (flag in bit 31)
   const uint64_t carry = (sex >> 31) ? (sex & 0x7FFFFFFFull) : tcarry + (sex & 0x7FFFFFFFull);
@@ -375,9 +382,9 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
     if (r) return (uint64_t)popc64(L & below & (~0ull << (63 - clz64(r))));
     return carry + popc64(L & below);
   };
-  if (has_lab) {
-    uint32_t nl = 0, nf = 0;
-    if (Lc == 0) {
+  if (has_sp) {
+    uint32_t nl = 0, nf = 0, nw = 0;
+    if (has_lab && Lc == 0) {
       // column-0 labels are the row starts holding a token; a row's first
       // delimiter is the first after its start (row starts are sparse)
       nl = (uint32_t)popc64(RS & T);
@@ -387,10 +394,12 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
         const uint64_t r = rs & (0ull - rs), nx = (rs & (rs - 1)) & (0ull - (rs & (rs - 1)));
         nf += (L & (nx ? nx - 1 : ~0ull) & ~(r | (r - 1))) != 0;
       }
-    } else {
+    } else if (has_lab) {
       for (uint64_t m = T; m; m &= m - 1) nl += col_of((uint32_t)ctz64(m)) == Lc;
     }
-    if (nl) atomic_add_u32(&sh.nlab, nl);
+    if (has_w)
+      for (uint64_t m = T; m; m &= m - 1) nw += col_of((uint32_t)ctz64(m)) == Wc;
+    if (nl | nw) atomic_add_u32(&sh.nlab, nl | (nw << 16));
     if (nf) atomic_add_u32(&sh.nfirst, nf);
     bk.sync();
     // only tiles whose rows straddle their ends add, into one of kLabShards
@@ -398,16 +407,18 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
     // MI355X_MICROARCH.md "dequeue")
     if (tid == 0) {
       uint64_t *sum = a.labsum + (uint64_t)(k % kLabShards) * 8;
-      if (sh.nlab != nR) atomic_add_u64(&sum[0], (uint64_t)sh.nlab - (uint64_t)nR);
+      const uint32_t tl = sh.nlab & 0xFFFFu, tw = sh.nlab >> 16;
+      if (has_lab && tl != nR) atomic_add_u64(&sum[0], (uint64_t)tl - (uint64_t)nR);
+      if (has_w && tw != nR) atomic_add_u64(&sum[2], (uint64_t)tw - (uint64_t)nR);
       if (Lc == 0 && sh.nfirst != nR) atomic_add_u64(&sum[1], (uint64_t)sh.nfirst - (uint64_t)nR);
     }
   }
   if (k + 1 == a.ntiles && tid == 0) {
-    const uint64_t rows = bRows + nR, vals = bVal + nT - (has_lab ? rows : 0);
+    const uint64_t rows = bRows + nR, vals = bVal + nT - rows * nsp;
     a.res[C_ROWS] = rows;
     a.res[C_INDEX] = vals;
     a.res[C_VALUE] = vals;
-    a.res[C_WEIGHT] = 0;
+    a.res[C_WEIGHT] = has_w ? rows : 0;
     a.res[C_QID] = 0;
     a.res[C_LABEL] = has_lab ? rows : 0;
     a.res[C_FIELD] = 0;
@@ -418,7 +429,8 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
   // ---- stores: values and column indices (labels), then row offsets
   auto put = [&](uint64_t g, uint32_t b, float v) {  // g: global token rank
     const uint64_t c = col_of(b);
-    if (has_lab) {
+    const uint64_t sp_before = (c > Lc ? 1u : 0u) + (c > Wc ? 1u : 0u);
+    if (has_sp) {
       const uint64_t bit = 1ull << b;
       const uint64_t row = eR + popc64(RS & ((bit - 1) | bit)) - 1;  // this token's row
       if (c == Lc) {
@@ -426,9 +438,14 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
         else raise_error(a.err, E_CAPACITY, P + b);
         return;
       }
-      g -= row + (c > Lc ? 1u : 0u);  // labels before this token
+      if (c == Wc) {
+        if (row < a.cap[C_WEIGHT]) a.weight[row] = v;
+        else raise_error(a.err, E_CAPACITY, P + b);
+        return;
+      }
+      g -= row * nsp + sp_before;  // labels and weights before this token
     }
-    const uint64_t ci = c - (c > Lc ? 1u : 0u);
+    const uint64_t ci = c - sp_before;
     if (g < a.cap[C_VALUE] && g < a.cap[C_INDEX]) {
       a.value[g] = v;
       if (a.wide) reinterpret_cast<uint64_t *>(a.index)[g] = ci;
@@ -437,7 +454,7 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
       raise_error(a.err, E_CAPACITY, P + b);
     }
   };
-  if (!has_lab) {
+  if (!has_sp) {
     // list entry j of the pass starting at token s0: value rank bVal + s0 + j
     auto put_tok = [&](uint64_t g, uint32_t e, float v) {
       const uint64_t ci = ((e >> 14) & ((1u << kColBits) - 1)) + ((e >> 31) ? tcarry : 0u);
@@ -486,7 +503,7 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
     uint64_t r = eR;
     for (uint64_t m = RS; m; m &= m - 1, ++r) {
       const int b = ctz64(m);
-      if (r < a.cap[C_ROWS]) a.offset[r] = eT + popc64(T & ((1ull << b) - 1)) - (has_lab ? r : 0);
+      if (r < a.cap[C_ROWS]) a.offset[r] = eT + popc64(T & ((1ull << b) - 1)) - r * nsp;
       else raise_error(a.err, E_CAPACITY, P + b);
     }
   }
@@ -499,8 +516,8 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
       uint64_t *row = a.chunk_tab + (uint64_t)(sh.c.c_first + i) * 8;
       const uint64_t rows = eR + popc64(RS & below);
       row[C_ROWS] = rows;
-      row[C_INDEX] = row[C_VALUE] = eT + popc64(T & below) - (has_lab ? rows : 0);
-      row[C_WEIGHT] = 0;
+      row[C_INDEX] = row[C_VALUE] = eT + popc64(T & below) - rows * nsp;
+      row[C_WEIGHT] = has_w ? rows : 0;
       row[C_QID] = 0;
       row[C_LABEL] = has_lab ? rows : 0;
       row[C_FIELD] = 0;

@@ -860,7 +860,7 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
   bk.sync();
   // a byte outside the grammar ('#' among them) in the tile or in the pre-halo:
   // blank the comments and classify again (block-uniform, libsvm only)
-  if (!FM && sh.hashy) bad = comments_reclassify(t, sh, bad, bk);
+  if (!FM && __builtin_expect(sh.hashy != 0, 0)) bad = comments_reclassify(t, sh, bad, bk);
   if (tid == 0) bad |= sh.c.toomany;
   FAST_STAMP(k, 3);
 #if defined(FSVM_ABL_STOP) && FSVM_ABL_STOP == 1  // timing ablation only: stage + classify

@@ -329,7 +329,8 @@ extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *c
     a.err = err;
     // mirrors launch_csv (csv.hip): uniform-grammar kernel first, exact tile
     // kernels when it sets the gate (or the parameters are outside its form)
-    const bool use_fast = nbytes > 0 && prm->value_type == DMLC_AMD_F32 && prm->weight_column < 0 &&
+    const bool use_fast = nbytes > 0 && prm->value_type == DMLC_AMD_F32 &&
+                          csv_fast_columns_ok(prm->label_column, prm->weight_column) &&
                           a.fast_delim && !(prm->flags & DMLC_AMD_FLAG_EXACT);
     uint32_t gate = use_fast ? 0u : 1u;
     std::vector<uint64_t> labsum_v(kLabShards * 8, 0);
@@ -348,7 +349,9 @@ extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *c
       f.wide = a.wide;
       f.delim = a.delim;
       f.label_col = prm->label_column;
+      f.weight_col = prm->weight_column;
       f.label = reinterpret_cast<float *>(out->label);
+      f.weight = out->weight;
       f.labsum = labsum;
       f.offset = out->offset;
       f.index = out->index;
@@ -362,17 +365,21 @@ extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *c
       for (uint64_t k = 0; k < nft; ++k) {
         fcsv::Shared *sh = new fcsv::Shared;
         std::memset(sh, 0xCD, sizeof(*sh));
-        if (count_only) run_block([&](HostBlock &bk) { fcsv::tile<1>(f, *sh, bk, (uint32_t)k); });
-        else run_block([&](HostBlock &bk) { fcsv::tile<2>(f, *sh, bk, (uint32_t)k); });
+        const bool sp = f.label_col >= 0 || f.weight_col >= 0;
+        if (count_only && sp) run_block([&](HostBlock &bk) { fcsv::tile<1, true>(f, *sh, bk, (uint32_t)k); });
+        else if (count_only) run_block([&](HostBlock &bk) { fcsv::tile<1, false>(f, *sh, bk, (uint32_t)k); });
+        else if (sp) run_block([&](HostBlock &bk) { fcsv::tile<2, true>(f, *sh, bk, (uint32_t)k); });
+        else run_block([&](HostBlock &bk) { fcsv::tile<2, false>(f, *sh, bk, (uint32_t)k); });
         delete sh;
       }
-      if (f.label_col >= 0) {  // label_check_kernel
-        uint64_t s0 = 0, s1 = 0;
+      if (f.label_col >= 0 || f.weight_col >= 0) {  // label_check_kernel
+        uint64_t s0 = 0, s1 = 0, s2 = 0;
         for (int i = 0; i < kLabShards; ++i) {
           s0 += labsum[i * 8];
           s1 += labsum[i * 8 + 1];
+          s2 += labsum[i * 8 + 2];
         }
-        if (s0 != 0 || s1 != 0) gate |= 1u;
+        if (s0 != 0 || s1 != 0 || s2 != 0) gate |= 1u;
       }
     }
     std::fprintf(stderr, "emu: csv path=%s\n", gate ? "exact" : "fast");

@@ -268,7 +268,7 @@ def libfm_rows(rng, rows, width, weights=False):
     return ("\n".join(out) + "\n").encode()
 
 
-def labeled_csv(rng, nlines, ncols, label_col, delim=",", defects=0.0):
+def labeled_csv(rng, nlines, ncols, label_col, delim=",", defects=0.0, weight_col=-1):
     """CSV with a label column: every row holds ncols non-empty numeric fields
     (the single-pass kernel's label form) unless a defect is injected with
     probability `defects`: an empty label field, a short row, a one-field row,
@@ -280,7 +280,7 @@ def labeled_csv(rng, nlines, ncols, label_col, delim=",", defects=0.0):
         if rng.random() < defects:
             kind = int(rng.integers(0, 5))
             if kind == 0:
-                fields[min(label_col, ncols - 1)] = ""
+                fields[min(weight_col if weight_col >= 0 and rng.random() < 0.5 else label_col, ncols - 1)] = ""
             elif kind == 1:
                 fields = fields[:int(rng.integers(1, max(2, label_col + 1)))]
             elif kind == 2:

@@ -412,3 +412,31 @@ def test_emu_comments_across_tile_ends(body):
             com = (b"#" + (body.encode() * (L // len(body) + 1))[:L]).replace(b"\n", b" ")
             data = pre + com + b"\n" + base[cut:]
             _emu_vs_oracle(data, [0, len(data)] if (d + L) % 2 else [0, cut, len(data)])
+
+
+def test_emu_csv_fast_weight_column():
+    """weight_column (csv_parser.h:113-114) on the single-pass CSV kernel,
+    alone and with a label column: clean inputs stay on it; empty weights,
+    short rows and the column forms where a row of special fields is fatal
+    (weight column 0, {label, weight} = {0, 1}) go to the exact kernels --
+    the reference's result (or error) either way."""
+    rng = np.random.default_rng(9090)
+    fast = 0
+    combos = [(-1, 1), (-1, 3), (0, 2), (3, 1), (1, 4), (2, 0), (0, 1), (-1, 0)]
+    for it in range(32):
+        lc, wc = combos[it % len(combos)]
+        nl = 400 if it % 8 == 7 else int(rng.integers(1, 40))
+        data = fuzz_text.labeled_csv(rng, nl, int(rng.integers(max(lc, wc) + 2, max(lc, wc) + 12)), lc,
+                                     defects=0.0 if it % 16 < 8 else 0.1, weight_col=wc)
+        offs = fuzz_text.random_cuts(rng, data, 4)
+        kw = dict(label_column=lc, weight_column=wc)
+        o = po.parse_chunks(data, offs, fmt=po.CSV, **kw)
+        h = pyemu.parse(data, offs, "csv", **kw)
+        failed = check_fail(h, "csv", offs)
+        assert (o["status"] != 0) == failed, (it, lc, wc, o["msg"], h["error"])
+        if not failed:
+            assert diff(h, o) == [], (it, lc, wc, diff(h, o))
+        if it % 16 < 8 and it % 8 < 5:
+            assert h["path"] == "fast", (it, lc, wc)
+        fast += h["path"] == "fast"
+    assert fast >= 10

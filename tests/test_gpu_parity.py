@@ -367,6 +367,28 @@ def test_gpu_comment_bench_size_fast_equals_exact(dm):
                            b.view(torch.int32) if b.dtype == torch.float32 else b), k
 
 
+def test_gpu_csv_fast_weight_column_vs_oracle(dm):
+    """weight_column on the single-pass CSV kernel (csv_fast_tile_sp), alone
+    and with a label column; the forms it leaves to the exact kernels (weight
+    column 0, {label, weight} = {0, 1}, empty weights, short rows) -- both
+    paths equal the oracle."""
+    rng = np.random.default_rng(9191)
+    paths = {"fast": 0, "exact": 0}
+    combos = [(-1, 1), (-1, 3), (0, 2), (3, 1), (1, 4), (2, 0), (0, 1), (-1, 0)]
+    for it in range(96):
+        lc, wc = combos[it % len(combos)]
+        nl = 3000 if it % 16 == 7 else int(rng.integers(1, 60))
+        data = fuzz_text.labeled_csv(rng, nl, int(rng.integers(max(lc, wc) + 2, max(lc, wc) + 40)), lc,
+                                     defects=0.0 if it % 16 < 8 else 0.1, weight_col=wc)
+        offs = fuzz_text.random_cuts(rng, data, int(rng.integers(0, 6)))
+        h = _gpu_vs_oracle_paths(dm, data, offs, fmt=po.CSV, label_column=lc, weight_column=wc,
+                                 **({"index_bits": 64} if it % 5 == 1 else {}))
+        paths[h["path"]] += 1
+        if it % 16 < 8 and it % 8 < 5:
+            assert h["path"] == "fast", (it, lc, wc)
+    assert paths["fast"] >= 30 and paths["exact"] >= 20, paths
+
+
 def test_gpu_qid_bench_size_fast_equals_exact(dm):
     """The qid bench config (1M rows x 128 nnz, qid:<row/16> on every row):
     single-pass == exact bit for bit, qid[r] = r / 16."""
