@@ -41,6 +41,16 @@ CONFIGS = {
     "libfm_1m_x64": ("libfm", 1 << 20, 64, None),  # SURVEY 8(f) row 3, not a BASELINE config
     "libsvm_qid_1m_x128": ("libsvm_qid", 1 << 20, 128, None),  # config 2's rows with qid: (ranking data)
     "libsvm_cmt_1m_x128": ("libsvm_cmt", 1 << 20, 128, None),  # config 2's rows with '#' comments
+    # grammar variants of configs 2 / 3 (the rates real data hits
+    # off the canonical shape)
+    "libsvm_im1_1m_x128": ("libsvm", 1 << 20, 128, None),  # config 2 with ?indexing_mode=-1
+    "csv_i32_1m_x256": ("csv", 1 << 20, 256, None),        # config 3 parsed as Parser<uint32_t, int32_t>
+    "csv_sp_1m_x256": ("csv_sp", 1 << 20, 256, None),      # config 3 with ", " between values
+}
+# parser arguments per config (dmlc_amd_params; the reference's URI args)
+PARAMS = {
+    "libsvm_im1_1m_x128": {"indexing_mode": -1},
+    "csv_i32_1m_x256": {"value_type": "i32"},
 }
 DESC = {
     "libsvm_1m_x128": "libsvm 1M rows x 128 nnz/row, device-resident",
@@ -50,14 +60,17 @@ DESC = {
     "libfm_1m_x64": "libfm 1M rows x 64 field:id:value/row, device-resident",
     "libsvm_qid_1m_x128": "libsvm 1M rows x 128 nnz/row with qid:<row/16> on every row, device-resident",
     "libsvm_cmt_1m_x128": "libsvm 1M rows x 128 nnz/row, a '# row <r>' comment on every row and a header, device-resident",
+    "libsvm_im1_1m_x128": "libsvm 1M rows x 128 nnz/row, indexing_mode=-1 (per-range 1-based detection), device-resident",
+    "csv_i32_1m_x256": "CSV dense 1M rows x 256 cols parsed with DType int32 (strtoll), device-resident",
+    "csv_sp_1m_x256": "CSV dense 1M rows x 256 float cols, ', ' separators, device-resident",
 }
 SYNTH = {"libsvm": synth.LIBSVM, "csv": synth.CSV, "libfm": synth.LIBFM, "libsvm_qid": synth.LIBSVM_QID,
-         "libsvm_cmt": synth.LIBSVM_CMT}
+         "libsvm_cmt": synth.LIBSVM_CMT, "csv_sp": synth.CSV_SP}
 # the arithmetic the path computes in (values decoded to f32 through the
 # reference's f64 fraction divide; indices / fields as u32)
 DTYPE = {"libsvm": "f32 values / u32 index", "libsvm_qid": "f32 values / u32 index / u64 qid",
          "libsvm_cmt": "f32 values / u32 index",
-         "csv": "f32 values", "libfm": "f32 values / u32 index / u32 field"}
+         "csv": "f32 values", "csv_sp": "f32 values", "libfm": "f32 values / u32 index / u32 field"}
 
 
 def log(*a):
@@ -123,6 +136,29 @@ def cpu_baseline(text, starts, fmt, budget_s, wide=False):
                          nproc, secs)}
 
 
+def spawn_ranks(n):
+    """`bench.py --gpus N` without a launcher: start N rank processes (one per
+    GPU) the way torch.distributed.run would, and exit with the first failing
+    rank's status.  The parent makes no GPU call (device_count does not
+    initialise the GPU on this image), so the children own their devices."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DMLC_AMD_BENCH_SPAWNED="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    for pr in procs:
+        c = pr.wait()
+        if c and not rc:
+            rc = c
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -137,20 +173,29 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
+
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and not (world == 1 and args.gpus == 1):
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE %d" % (args.gpus, world))
     dist = None
+    backend = None
+    ndev = torch.cuda.device_count()
     if world > 1:
         import torch.distributed as dist
-        ndev = torch.cuda.device_count()
         if ndev >= world:  # one process per GPU: RCCL for the barriers and the max-over-ranks time
             torch.cuda.set_device(local)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:  # rehearsal with more ranks than GPUs (ranks share a card): gloo on the host
             torch.cuda.set_device(local % ndev)
             dist.init_process_group("gloo")
+        backend = dist.get_backend()
+        if dist.get_world_size() != args.gpus:
+            raise SystemExit("bench.py: process group has %d ranks, --gpus %d" % (dist.get_world_size(), args.gpus))
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -169,15 +214,18 @@ def main():
     d_text = torch.from_numpy(text).to(dev)
     d_starts = torch.from_numpy(starts).to(dev)
     nbytes = int(text.size)
-    pkw = {"label_column": args.label_column} if fmt == "csv" else {}
-    pfmt = "libsvm" if fmt in ("libsvm_qid", "libsvm_cmt") else fmt
+    pfmt = {"libsvm_qid": "libsvm", "libsvm_cmt": "libsvm", "csv_sp": "csv"}.get(fmt, fmt)
+    pkw = dict(PARAMS.get(args.config, {}))
+    if pfmt == "csv":
+        pkw["label_column"] = args.label_column
     p = dmlc_amd.DeviceParser(pfmt, tile_bytes=args.tile_bytes, **pkw)
     res = torch.zeros(16, dtype=torch.int64, device=dev)
     counts = p.count(d_text, d_starts, result=res)
     out = p.alloc(counts)
     out["_csr"] = p.csr_of(out)
-    b_out = csr_bytes(counts)
-    s = torch.cuda.current_stream()
+    vtype = pkw.get("value_type", "f32")
+    b_out = csr_bytes(counts, vbytes=8 if vtype == "i64" else 4)
+    dtype = DTYPE[fmt] if vtype == "f32" else "%s values (strtoll) / u32 index" % vtype
 
     def step():
         # one full dmlc_amd_parse call (flags 0) into pre-allocated outputs: the
@@ -238,6 +286,7 @@ def main():
             traffic = tr["hbm_bytes_per_launch"]
     except (OSError, ValueError):
         pass
+    par = "shard%d" % world
     line = {
         "metric": "device-resident libsvm parse GB/s (input bytes) at 1/2/4/8 GPU; % HBM roofline",
         "value": round(value, 3),
@@ -249,13 +298,14 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": DTYPE[fmt],
+        "dtype": dtype,
         "data": "synthetic (tools/synth.c splitmix64 seed 1, %.9g values), HBM-resident",
-        "config": {"workload": DESC[args.config], "baseline_config": cfg_idx, "format": fmt,
+        "config": {"workload": DESC[args.config], "baseline_config": cfg_idx, "format": pfmt,
                    "rows_per_gpu": rows, "width": width, "input_bytes_per_gpu": nbytes,
                    "csr_bytes_per_gpu": b_out, "nnz_per_gpu": int(counts[dmlc_amd.INDEX]),
-                   "chunks_per_gpu": len(starts) - 1, "parallelism": "shard%d" % world,
-                   **({"label_column": args.label_column} if args.label_column >= 0 else {})},
+                   "chunks_per_gpu": len(starts) - 1, "parallelism": par,
+                   **({"label_column": args.label_column} if args.label_column >= 0 else {}),
+                   **{k: v for k, v in pkw.items() if k != "label_column"}},
         "hbm_frac_input": round(value / world / HBM_PEAK_GBS, 4),
         "hbm_frac_in_out": round((total_in + b_out * world) * args.steps / elapsed / 1e9
                                  / world / HBM_PEAK_GBS, 4),
@@ -266,6 +316,11 @@ def main():
                      "bytes_per_launch": dom_bytes, "avg_ms": round(dom_ms, 4)},
         "cpu_baseline": None,
     }
+    if world > 1:
+        line["ranks"] = {"world_size": world, "backend": backend, "devices_visible": ndev,
+                         "launcher": "bench.py --gpus" if os.environ.get("DMLC_AMD_BENCH_SPAWNED") else "external",
+                         "note": "one rank per GPU" if ndev >= world else
+                                 "rehearsal: %d ranks share %d card(s), gloo barriers" % (world, ndev)}
     if rank == 0 and world == 1:
         try:
             line["hbm_copy"] = {"GBps": hbm_copy_rate(dev), "what": "torch device copy of 4 GiB, (read+write)/time"}

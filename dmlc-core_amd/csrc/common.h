@@ -75,6 +75,40 @@ struct Base64 {  // absolute 64-bit ranks
   uint64_t c[C_N];
 };
 
+// indexing_mode < 0 (libsvm_parser.h:165-171): the minimum index of the
+// ParseBlock unit a thread is walking, kept in registers and flushed to
+// chunk_min[unit] when the walk enters another unit and once per tile
+// (tile_min_flush), instead of one device atomic per index on a handful of
+// addresses (which serialised the count pass: 437 ms on config 2).
+struct MinAcc {
+  int unit = -1;
+  uint64_t v = ~0ull;
+  DA_HD void add(uint64_t *cmin, int u, uint64_t x) {
+    if (u != unit) {
+      flush(cmin);
+      unit = u;
+      v = x;
+    } else if (x < v) {
+      v = x;
+    }
+  }
+  DA_HD void flush(uint64_t *cmin) {
+    if (unit >= 0) atomic_min_u64((unsigned long long *)&cmin[unit], (unsigned long long)v);
+    unit = -1;
+    v = ~0ull;
+  }
+};
+// Block-wide: the threads on the block's lowest unit reduce first (one atomic
+// for the common tile inside one unit); any other unit flushes on its own.
+template <class BK>
+DA_HDF void tile_min_flush(MinAcc &m, uint64_t *cmin, BK &bk) {
+  const uint64_t u0 = bk.min_u64(m.unit >= 0 ? (uint64_t)m.unit : ~0ull);
+  const uint64_t m0 = bk.min_u64(m.unit >= 0 && (uint64_t)m.unit == u0 ? m.v : ~0ull);
+  if (bk.tid() == 0 && u0 != ~0ull) atomic_min_u64((unsigned long long *)&cmin[u0], (unsigned long long)m0);
+  if (m.unit >= 0 && (uint64_t)m.unit != u0) m.flush(cmin);
+  m.unit = -1;
+}
+
 // Record the first (lowest position) error: (pos << 16) | code, min wins.
 DA_HD void raise_error(unsigned long long *err, uint32_t code, uint64_t pos) {
   atomic_min_u64(err, ((unsigned long long)(pos & 0xFFFFFFFFFFFFull) << 16) | code);

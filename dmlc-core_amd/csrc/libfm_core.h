@@ -87,14 +87,14 @@ DA_HD uint64_t prev_run(const F &at, uint64_t x, uint64_t floor) {
 // st; MODE 1: count from concrete state st; MODE 2: count and emit.
 template <int MODE>
 DA_HDF void walk(const LibfmArgs &a, Src &src, const uint32_t *r1bits, uint64_t w0, const Seg &sg,
-                 uint32_t &st, Cnt &cnt, const Base64 &base) {
+                 uint32_t &st, Cnt &cnt, const Base64 &base, MinAcc *macc = nullptr) {
   uint32_t ev = sg.rs | sg.ls | sg.le;
   int chunk = sg.chunk;
   uint64_t cfloor = a.cs[chunk], cend = a.cs[chunk + 1];
   src.lim = a.lim(chunk);  // decoders read to the InputSplit chunk end
   // one (field, index) pair: decode, check signs, store / track the chunk minimum
   auto pair = [&](uint64_t fpos, uint64_t ipos, uint64_t x) {
-    if (MODE == 2 || a.indexing_mode < 0) {
+    if (MODE == 2 || macc) {
       uint64_t fv, iv;
       bool ok = parse_uint(src, fpos, a.wide != 0, &fv);
       ok = parse_uint(src, ipos, a.wide != 0, &iv) && ok;
@@ -103,7 +103,11 @@ DA_HDF void walk(const LibfmArgs &a, Src &src, const uint32_t *r1bits, uint64_t 
         fv = iv = 0;
       }
       if (MODE == 1) {
-        atomic_min_u64((unsigned long long *)&a.chunk_min[chunk], (unsigned long long)(fv < iv ? fv : iv));
+        if (!a.wide) {
+          fv = (uint32_t)fv;
+          iv = (uint32_t)iv;
+        }
+        macc->add(a.chunk_min, chunk, fv < iv ? fv : iv);
       } else {
         if (a.indexing_mode > 0 || (a.indexing_mode < 0 && a.chunk_min[chunk] > 0)) {
           --fv;
@@ -245,6 +249,8 @@ DA_HDF void tile(const LibfmArgs &a, svm::Shared &sh, BK &bk, uint64_t k) {
   int j = 0;             // window counter
   uint32_t st0 = S_PRE;  // concrete state at the window start
   bool done = false;
+  MinAcc macc;  // count pass, indexing_mode < 0: this thread's unit minimum
+  MinAcc *mp = MODE == 1 && a.indexing_mode < 0 ? &macc : nullptr;
   Src src;
   src.g = a.text;
   src.lds = sh.win;
@@ -342,7 +348,7 @@ DA_HDF void tile(const LibfmArgs &a, svm::Shared &sh, BK &bk, uint64_t k) {
     Cnt c = zero;
     if (sg.lo < sg.hi) {
       uint32_t s2 = st;
-      walk<1>(a, src, sh.r1bits, w0, sg, s2, c, nob);
+      walk<1>(a, src, sh.r1bits, w0, sg, s2, c, nob, mp);
     }
     if (MODE == 1) {
       mine = CntAdd()(mine, c);
@@ -363,6 +369,7 @@ DA_HDF void tile(const LibfmArgs &a, svm::Shared &sh, BK &bk, uint64_t k) {
     ++j;
     bk.sync();
   }
+  if (mp) tile_min_flush(macc, a.chunk_min, bk);
   if (MODE == 1) {
     Cnt total;
     (void)bk.exclusive(mine, zero, CntAdd(), &total);

@@ -126,7 +126,7 @@ DA_HD bool r1_bit(const uint32_t *bits, uint64_t w0, uint64_t x) {
 // and emit (decode + store at base + local rank).
 template <int MODE>
 DA_HDF void walk(const LibsvmArgs &a, Src &src, const uint32_t *r1bits, uint64_t w0, const Seg &sg,
-                 uint32_t &st, Cnt &cnt, const Base64 &base) {
+                 uint32_t &st, Cnt &cnt, const Base64 &base, MinAcc *macc = nullptr) {
   uint32_t ev = sg.rs | sg.ls | sg.le;
   int chunk = sg.chunk;
   uint64_t cfloor = a.cs[chunk], cend = a.cs[chunk + 1];
@@ -213,14 +213,14 @@ DA_HDF void walk(const LibsvmArgs &a, Src &src, const uint32_t *r1bits, uint64_t
           }
         }
         if (role == 1) {
-          if (MODE == 2 || a.indexing_mode < 0) {
+          if (MODE == 2 || macc) {
             uint64_t v;
             if (!parse_uint(src, x, a.wide != 0, &v)) {
               raise_error(a.err, E_NEG_INDEX, x);
               v = 0;
             }
             if (MODE == 1) {
-              atomic_min_u64((unsigned long long *)&a.chunk_min[chunk], (unsigned long long)v);
+              macc->add(a.chunk_min, chunk, a.wide ? v : (uint64_t)(uint32_t)v);
             } else {
               if (a.indexing_mode > 0 || (a.indexing_mode < 0 && a.chunk_min[chunk] > 0)) --v;
               const uint64_t ir = base.c[C_INDEX] + cnt.c[C_INDEX];
@@ -313,6 +313,8 @@ DA_HDF void tile(const LibsvmArgs &a, Shared &sh, BK &bk, uint64_t k) {
   int j = 0;             // window counter
   uint32_t st0 = S_PRE;  // concrete role state at the window start
   bool done = false;
+  MinAcc macc;  // count pass, indexing_mode < 0: this thread's unit minimum
+  MinAcc *mp = MODE == 1 && a.indexing_mode < 0 ? &macc : nullptr;
   Src src;
   src.g = a.text;
   src.lds = sh.win;
@@ -413,7 +415,7 @@ DA_HDF void tile(const LibsvmArgs &a, Shared &sh, BK &bk, uint64_t k) {
     Cnt c = zero;
     if (sg.lo < sg.hi) {
       uint32_t s2 = st;
-      walk<1>(a, src, sh.r1bits, w0, sg, s2, c, nob);
+      walk<1>(a, src, sh.r1bits, w0, sg, s2, c, nob, mp);
     }
     if (MODE == 1) {
       mine = CntAdd()(mine, c);
@@ -434,6 +436,7 @@ DA_HDF void tile(const LibsvmArgs &a, Shared &sh, BK &bk, uint64_t k) {
     ++j;
     bk.sync();
   }
+  if (mp) tile_min_flush(macc, a.chunk_min, bk);
   if (MODE == 1) {
     Cnt total;
     (void)bk.exclusive(mine, zero, CntAdd(), &total);

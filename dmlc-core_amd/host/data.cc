@@ -234,13 +234,17 @@ struct Page {
            index.size() * sizeof(I) + value.size() * sizeof(D);
   }
   // row_block.h:126-168; a block without labels (label-less CSV) pushes zeros
-  // where the reference copies from its NULL label pointer
-  void Push(const dmlc::RowBlock<I, D> &b) {
+  // where the reference copies from its NULL label pointer.  With the block's
+  // counts known (this build's parser, k) only its own weights / qids are
+  // read: a libsvm block where some rows lack label:weight or qid: holds fewer
+  // of them than rows, and the reference's `size` of them would read past the
+  // block's share of the pinned batch arrays.
+  void Push(const dmlc::RowBlock<I, D> &b, const BlockCounts *k = nullptr) {
     const size_t n0 = label.size();
     label.resize(n0 + b.size);
     if (b.label) std::memcpy(label.data() + n0, b.label, b.size * sizeof(D));
-    if (b.weight) weight.insert(weight.end(), b.weight, b.weight + b.size);
-    if (b.qid) qid.insert(qid.end(), b.qid, b.qid + b.size);
+    if (b.weight) weight.insert(weight.end(), b.weight, b.weight + (k ? k->weights : b.size));
+    if (b.qid) qid.insert(qid.end(), b.qid, b.qid + (k ? k->qids : b.size));
     const size_t ndata = b.offset[b.size] - b.offset[0];
     if (b.field) {
       field.insert(field.end(), b.field, b.field + ndata);
@@ -330,8 +334,9 @@ class HipDiskRowIter : public dmlc::RowBlockIter<I, D> {
     std::unique_ptr<dmlc::Stream> fo(dmlc::Stream::Create(cache_file_.c_str(), "w"));
     Page<I, D> data;
     num_col_ = 0;
+    auto *hp = dynamic_cast<HipTextParser<I, D> *>(parser);
     while (parser->Next()) {
-      data.Push(parser->Value());
+      data.Push(parser->Value(), hp ? &hp->ValueCounts() : nullptr);
       if (data.MemCostBytes() >= kPageSize) {
         num_col_ = std::max(num_col_, static_cast<size_t>(data.max_index) + 1);
         data.Save(fo.get());

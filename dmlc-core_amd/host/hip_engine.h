@@ -444,12 +444,17 @@ class HipTextParser : public dmlc::Parser<IndexType, DType> {
  private:
   struct Worker {
     explicit Worker(int d) : device(d) {}
+    // runs on whichever thread destroys the parser: switch to the worker's
+    // device for its stream and events, then give the caller its device back
     ~Worker() {
       if (stream) {
+        int prev = -1;
+        const bool have_prev = hipGetDevice(&prev) == hipSuccess;
         (void)hipSetDevice(device);
         for (auto &e : ev)
           if (e) (void)hipEventDestroy(e);
         (void)hipStreamDestroy(stream);
+        if (have_prev && prev != device) (void)hipSetDevice(prev);
       }
     }
     int device;

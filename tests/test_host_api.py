@@ -388,3 +388,26 @@ def test_api_multi_device_dispatch(tmp_path):
         assert diff(hi, o) == [] and int(hi["meta"][2]) == int(o["index"].max()) + 1, devs
     bad = run_api(tmp_path, d, env={"DMLC_AMD_DEVICES": "99"})
     assert "no HIP device" in bad["error"]
+
+
+@pytest.mark.gpu
+def test_api_disk_row_cache_partial_weights_and_qids(tmp_path):
+    """uri#cachefile over libsvm blocks where only some rows carry label:weight
+    or qid: (fewer weights / qids than rows in a block): the cache pages hold
+    exactly the block's own weights and qids (no read past the block's share
+    of the batch arrays) and iterate back equal to the oracle's parse."""
+    lines = []
+    for i in range(30000):
+        lab = b"%d:0.%d" % (i % 2, 1 + i % 9) if i % 3 == 0 else b"%d" % (i % 2)
+        q = b" qid:%d" % (i // 7) if i % 5 == 0 else b""
+        lines.append(lab + q + b" %d:1.5 %d:2.25\n" % (i % 11, 20 + i % 13))
+    contents = [b"".join(lines)]
+    d, _ = _write(tmp_path / "pw", contents)
+    cache = str(tmp_path / "pw.cache")
+    h = run_api(tmp_path, d + "#" + cache, iter_=True)
+    o, _ = oracle_files(contents)
+    assert "error" not in h, h
+    assert len(h["weight"]) == len(o["weight"]) == 10000 and len(h["qid"]) == len(o["qid"]) == 6000
+    assert diff(h, o) == []
+    again = run_api(tmp_path, d + "#" + cache, iter_=True)  # the cache reused
+    assert diff(again, o) == []

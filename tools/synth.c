@@ -16,6 +16,8 @@
  *    row with q = row / 16 (ranking data, libsvm_parser.h:119-132).
  *  libsvm+comment row (fmt 4): the libsvm row with a trailing comment
  *    " # row <r>" (libsvm_parser.h:67-83), and a '#' header line first.
+ *  CSV+blank row (fmt 5): the CSV row with ", " between values (ParseFloat
+ *    skips the blank before each value, strtonum.h:95-264).
  */
 #include <stdint.h>
 #include <stdio.h>
@@ -68,13 +70,13 @@ static size_t fmt_libfm_row(char *o, uint64_t seed, uint64_t r, int K) {
   return (size_t)(p - o);
 }
 
-static size_t fmt_csv_row(char *o, uint64_t seed, uint64_t r, int C) {
+static size_t fmt_csv_row(char *o, uint64_t seed, uint64_t r, int C, int blank) {
   uint64_t s = row_state(seed, r);
   char *p = o;
   for (int j = 0; j < C; ++j) {
     uint64_t x = sm64(&s);
     float v = (float)(x >> 40) * (1.0f / 8388608.0f) - 1.0f;
-    p += sprintf(p, j ? ",%.9g" : "%.9g", (double)v);
+    p += sprintf(p, j ? (blank ? ", %.9g" : ",%.9g") : "%.9g", (double)v);
   }
   *p++ = '\n';
   return (size_t)(p - o);
@@ -83,7 +85,7 @@ static size_t fmt_csv_row(char *o, uint64_t seed, uint64_t r, int C) {
 /* upper bound on the bytes of `nrows` rows */
 size_t synth_bound(int fmt, uint64_t nrows, int width) {
   return fmt == 0 || fmt == 3 || fmt == 4 ? nrows * (size_t)(2 + 28 + width * 26) + 32
-                  : fmt == 2 ? nrows * (size_t)(2 + width * 30) : nrows * (size_t)(width * 18 + 2);
+                  : fmt == 2 ? nrows * (size_t)(2 + width * 30) : nrows * (size_t)(width * 19 + 2);
 }
 
 /* Format rows [row0, row0+nrows) into out (capacity cap); returns bytes, or 0
@@ -107,7 +109,7 @@ size_t synth_rows(int fmt, uint64_t row0, uint64_t nrows, int width, uint64_t se
       if (fmt == 4 && row0 + r == 0) n += (size_t)sprintf(buf + n, "# label id:value ... # row r\n");
       n += fmt == 0 || fmt == 3 || fmt == 4 ? fmt_libsvm_row(buf + n, seed, row0 + r, width, fmt == 3, fmt == 4)
                     : fmt == 2 ? fmt_libfm_row(buf + n, seed, row0 + r, width)
-                               : fmt_csv_row(buf + n, seed, row0 + r, width);
+                               : fmt_csv_row(buf + n, seed, row0 + r, width, fmt == 5);
     }
     bbuf[b] = buf;
     bsz[b] = n;
