@@ -70,6 +70,8 @@ struct FastSvmArgs {
   uint64_t *chunk_tab;  // may be null
   uint64_t *lb;         // look-back records [5 ntiles] (status words zeroed per launch)
   uint64_t *qsum;       // libsvm: qid runs, sharded by tile [kLabShards][8] (zeroed per launch)
+  uint64_t *umin;       // indexing_mode < 0: minimum stored index (libfm: and field) per ParseBlock
+                        // unit [nchunk], ~0 = none; filled by the write pass (svm_fast.h umin_fix)
   uint32_t *gate;       // != 0: input left the grammar -> exact path
   unsigned long long *err;  // first error of this path
   uint64_t *res;        // dmlc_amd_result counts (written by the last tile)
@@ -94,7 +96,8 @@ struct FastCsvArgs {
   uint64_t *labsum;     // [kLabShards][8], zeroed per launch: words 0/1/2 = sum(labels - rows),
                         // sum(first delimiters - rows), sum(weights - rows), sharded by tile (csv_fast.h)
   void *index;
-  float *value;
+  void *value;          // DType: float, or int32 / int64 (vtype)
+  int vtype;            // 0 f32, 1 i32, 2 i64 (integer values: csv_fast_tile_int)
   uint64_t cap[8];
   uint64_t *chunk_tab;  // may be null
   uint64_t *lb;
@@ -114,6 +117,10 @@ DA_HD bool csv_fast_columns_ok(int label_col, int weight_col) {
   if (weight_col == label_col || weight_col == 0) return false;
   return label_col < 0 || (label_col > weight_col ? label_col : weight_col) >= 2;
 }
+
+// The single-pass integer-DType kernel: no label column; the weight column
+// is an ordinary column for integer DTypes (csv_parser.h:111-114).
+DA_HD bool csv_fast_int_ok(int label_col) { return label_col < 0; }
 
 struct CsvArgs {
   const uint8_t *text;

@@ -66,6 +66,38 @@ struct DevBlock {
     return r;
   }
 
+  // inclusive prefix sum of 32-bit lanes over the wave by DPP (GFX9 forms:
+  // row_shr inside rows of 16, then row_bcast:15 / row_bcast:31 across rows),
+  // six VALU adds instead of six LDS permutes
+  __device__ __forceinline__ static uint32_t wave_incl_add(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);  // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);  // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);  // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);  // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);  // row_bcast:31
+    return x;
+  }
+  // Exclusive prefix sum and block total of packed counters whose fields
+  // never carry across bit 31 (the tiles' 16-bit role counts): two 32-bit
+  // DPP wave scans, one LDS round for the wave totals.
+  __device__ __forceinline__ uint64_t exclusive_add(uint64_t v, uint64_t *total) const {
+    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+    const uint64_t inc = wave_incl_add((uint32_t)v) | ((uint64_t)wave_incl_add((uint32_t)(v >> 32)) << 32);
+    if (lane == kWave - 1) scratch[wid] = inc;
+    __syncthreads();
+    uint64_t pre = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) {
+      const uint64_t t = scratch[w];
+      pre += w < wid ? t : 0;
+      tot += t;
+    }
+    *total = tot;
+    __syncthreads();
+    return pre + inc - v;
+  }
+
   // Exclusive prefix (identity for thread 0) and the block total.
   template <typename T, typename Op>
   __device__ __forceinline__ T exclusive(T v, T identity, Op op, T *total) const {

@@ -134,7 +134,7 @@ size_t dmlc_amd_workspace_bytes(uint64_t nbytes, int nchunks, const dmlc_amd_par
   const uint64_t ntiles = (nbytes + T - 1) / T;
   const uint64_t nc = (nchunks > 0 ? (uint64_t)nchunks : 1) * (uint64_t)units_per_chunk(prm);
   const uint64_t nft = (nbytes + kFastTile - 1) / kFastTile;
-  return (size_t)((2 * ntiles * kSlots + nc + nc * 8 + (nc + 1) + nft * 8 + dmlc_amd::kLabShards * 8) *
+  return (size_t)((2 * ntiles * kSlots + 2 * nc + nc * 8 + (nc + 1) + nft * 8 + dmlc_amd::kLabShards * 8) *
                       sizeof(uint64_t) +
                   12 * 256);
 }
@@ -166,6 +166,7 @@ int dmlc_amd_parse(const void *d_text, uint64_t nbytes, const uint64_t *d_chunk_
   uint64_t *tile_cnt = cv.take<uint64_t>(ntiles * kSlots + 1);
   uint64_t *tile_base = cv.take<uint64_t>(ntiles * kSlots + 1);
   uint64_t *chunk_min = cv.take<uint64_t>(nc);
+  uint64_t *fast_min = cv.take<uint64_t>(nc);  // single-pass write pass, indexing_mode < 0 (svm_fast.h umin_fix)
   uint64_t *chunk_sink = cv.take<uint64_t>((size_t)nc * 8);
   uint64_t *units = cv.take<uint64_t>((size_t)nc + 1);  // ParseBlock unit starts (nthread > 1)
   const uint64_t nft = (nbytes + kFastTile - 1) / kFastTile;
@@ -173,7 +174,7 @@ int dmlc_amd_parse(const void *d_text, uint64_t nbytes, const uint64_t *d_chunk_
   unsigned long long *ferr = cv.take<unsigned long long>(1);
   uint64_t *lb = cv.take<uint64_t>(nft * 8 + 1);
   uint64_t *labsum = cv.take<uint64_t>(dmlc_amd::kLabShards * 8);
-  if (!tile_cnt || !tile_base || !chunk_min || !chunk_sink || !units || !ctl || !ferr || !lb || !labsum)
+  if (!tile_cnt || !tile_base || !chunk_min || !fast_min || !chunk_sink || !units || !ctl || !ferr || !lb || !labsum)
     return DMLC_AMD_ERR_ARG;
   // FillData's thread ranges become the units the kernels parse; the
   // decoders still read to the end of the InputSplit chunk (args.h UnitLim)
@@ -237,13 +238,16 @@ int dmlc_amd_parse(const void *d_text, uint64_t nbytes, const uint64_t *d_chunk_
     f.index = a.index;
     f.value = a.value;
     for (int i = 0; i < 8; ++i) f.cap[i] = out->cap[i];
-    f.chunk_tab = d_chunk_table;
+    // indexing_mode < 0 needs the units' index ranges after the write pass:
+    // the chunk table, or the workspace's when the caller passes none
+    f.chunk_tab = d_chunk_table ? d_chunk_table : (prm->indexing_mode < 0 ? chunk_sink : nullptr);
     f.lb = lb;
     f.qsum = labsum;
+    f.umin = fast_min;
     f.gate = ctl;
     f.err = ferr;
     f.res = res;
-    const bool use_fast = nbytes > 0 && prm->indexing_mode >= 0 && !(prm->flags & DMLC_AMD_FLAG_EXACT);
+    const bool use_fast = nbytes > 0 && !(prm->flags & DMLC_AMD_FLAG_EXACT);
     e = dmlc_amd::launch_libsvm(a, f, use_fast, res, phase, s);
   } else if (prm->format == DMLC_AMD_CSV) {
     dmlc_amd::CsvArgs a;
@@ -283,24 +287,28 @@ int dmlc_amd_parse(const void *d_text, uint64_t nbytes, const uint64_t *d_chunk_
     f.delim = a.delim;
     f.skip_if_gated = phase == dmlc_amd::kPhaseFill;
     f.label_col = prm->label_column;
-    f.weight_col = prm->weight_column;
+    // the weight column is ordinary for integer DTypes (csv_parser.h:113-114)
+    f.weight_col = prm->value_type == DMLC_AMD_F32 ? prm->weight_column : -1;
+    f.vtype = prm->value_type;
     f.label = reinterpret_cast<float *>(out->label);
     f.weight = out->weight;
     f.labsum = labsum;
     f.offset = a.offset;
     f.index = a.index;
-    f.value = reinterpret_cast<float *>(a.value);
+    f.value = a.value;
     for (int i = 0; i < 8; ++i) f.cap[i] = out->cap[i];
     f.chunk_tab = d_chunk_table;
     f.lb = lb;
     f.gate = ctl;
     f.err = ferr;
     f.res = res;
-    // the uniform-grammar CSV kernel: float values, label / weight columns it
-    // takes, a delimiter the number decoder cannot consume (csv_fast.h)
-    const bool use_fast = nbytes > 0 && prm->value_type == DMLC_AMD_F32 &&
-                          dmlc_amd::csv_fast_columns_ok(prm->label_column, prm->weight_column) &&
-                          a.fast_delim && !(prm->flags & DMLC_AMD_FLAG_EXACT);
+    // the uniform-grammar CSV kernels: float values with the label / weight
+    // columns they take, or integer values without a label column; a
+    // delimiter the number decoders cannot consume (csv_fast.h)
+    const bool cols_ok = prm->value_type == DMLC_AMD_F32
+                             ? dmlc_amd::csv_fast_columns_ok(prm->label_column, prm->weight_column)
+                             : dmlc_amd::csv_fast_int_ok(prm->label_column);
+    const bool use_fast = nbytes > 0 && cols_ok && a.fast_delim && !(prm->flags & DMLC_AMD_FLAG_EXACT);
     e = dmlc_amd::launch_csv(a, f, use_fast, res, phase, s);
   } else {  // DMLC_AMD_LIBFM
     dmlc_amd::LibfmArgs a;
@@ -344,12 +352,13 @@ int dmlc_amd_parse(const void *d_text, uint64_t nbytes, const uint64_t *d_chunk_
     f.field = a.field;
     f.value = a.value;
     for (int i = 0; i < 8; ++i) f.cap[i] = out->cap[i];
-    f.chunk_tab = d_chunk_table;
+    f.chunk_tab = prm->indexing_mode < 0 ? a.chunk_tab : d_chunk_table;  // as libsvm's
     f.lb = lb;
+    f.umin = fast_min;
     f.gate = ctl;
     f.err = ferr;
     f.res = res;
-    const bool use_fast = nbytes > 0 && prm->indexing_mode >= 0 && !(prm->flags & DMLC_AMD_FLAG_EXACT);
+    const bool use_fast = nbytes > 0 && !(prm->flags & DMLC_AMD_FLAG_EXACT);
     e = dmlc_amd::launch_libfm(a, f, use_fast, res, phase, s);
   }
   if (e == hipSuccess && (prm->flags & DMLC_AMD_FLAG_MAX_INDEX) && phase != dmlc_amd::kPhaseCount) {

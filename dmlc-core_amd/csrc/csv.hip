@@ -17,6 +17,9 @@ __global__ void __launch_bounds__(kThreads) csv_tile(CsvArgs a) {
   csv::tile<MODE>(a, sh, bk, blockIdx.x);
 }
 
+// 6 workgroups per CU: LDS in 512-byte granules, <= 53 of them (svm_fast_tile)
+static_assert(sizeof(fcsv::Shared) + kBlockScratchU64 * 8 <= 53 * 512, "csv_fast_tile LDS above the 6-workgroup budget");
+
 #ifndef FCSV_MINW
 #define FCSV_MINW 6
 #endif
@@ -25,7 +28,15 @@ __global__ void __launch_bounds__(kThreads, FCSV_MINW) csv_fast_tile(FastCsvArgs
   __shared__ __attribute__((aligned(16))) fcsv::Shared sh;
   __shared__ uint64_t scratch[kBlockScratchU64];
   DevBlock bk{scratch};
-  fcsv::tile<MODE, false>(a, sh, bk, blockIdx.x);
+  fcsv::tile<MODE, false, 0>(a, sh, bk, blockIdx.x);
+}
+// integer DTypes (strtoll)
+template <int MODE>
+__global__ void __launch_bounds__(kThreads, FCSV_MINW) csv_fast_tile_int(FastCsvArgs a) {
+  __shared__ __attribute__((aligned(16))) fcsv::Shared sh;
+  __shared__ uint64_t scratch[kBlockScratchU64];
+  DevBlock bk{scratch};
+  fcsv::tile<MODE, false, 1>(a, sh, bk, blockIdx.x);
 }
 // with a label and / or weight column
 template <int MODE>
@@ -33,7 +44,7 @@ __global__ void __launch_bounds__(kThreads, FCSV_MINW) csv_fast_tile_sp(FastCsvA
   __shared__ __attribute__((aligned(16))) fcsv::Shared sh;
   __shared__ uint64_t scratch[kBlockScratchU64];
   DevBlock bk{scratch};
-  fcsv::tile<MODE, true>(a, sh, bk, blockIdx.x);
+  fcsv::tile<MODE, true, 0>(a, sh, bk, blockIdx.x);
 }
 
 // fill phase after a count phase that fell back to the exact kernels: reopen
@@ -89,14 +100,17 @@ hipError_t launch_csv(const CsvArgs &a, const FastCsvArgs &f, bool use_fast, uin
         (e = hipMemsetAsync(f.labsum, 0, kLabShards * 8 * sizeof(uint64_t), s)) != hipSuccess)
       return e;
     const bool sp = f.label_col >= 0 || f.weight_col >= 0;
+    const bool iv = f.vtype != 0;
     if (phase == kPhaseCount) {
-      prof_mark(0, s, "csv_fast_tile<1>");
-      if (sp) csv_fast_tile_sp<1><<<f.ntiles, kThreads, 0, s>>>(f);
+      prof_mark(0, s, iv ? "csv_fast_tile_int<1>" : "csv_fast_tile<1>");
+      if (iv) csv_fast_tile_int<1><<<f.ntiles, kThreads, 0, s>>>(f);
+      else if (sp) csv_fast_tile_sp<1><<<f.ntiles, kThreads, 0, s>>>(f);
       else csv_fast_tile<1><<<f.ntiles, kThreads, 0, s>>>(f);
       prof_mark(1, s, "csv_fast_tile<1>");
     } else {
-      prof_mark(0, s, "csv_fast_tile<2>");
-      if (sp) csv_fast_tile_sp<2><<<f.ntiles, kThreads, 0, s>>>(f);
+      prof_mark(0, s, iv ? "csv_fast_tile_int<2>" : "csv_fast_tile<2>");
+      if (iv) csv_fast_tile_int<2><<<f.ntiles, kThreads, 0, s>>>(f);
+      else if (sp) csv_fast_tile_sp<2><<<f.ntiles, kThreads, 0, s>>>(f);
       else csv_fast_tile<2><<<f.ntiles, kThreads, 0, s>>>(f);
       prof_mark(1, s, "csv_fast_tile<2>");
     }

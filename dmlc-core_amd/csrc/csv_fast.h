@@ -22,6 +22,8 @@
 //
 // Same structure and block policy as svm_fast.h (the CPU emulator runs it).
 #pragma once
+#include <type_traits>
+
 #include "fast_common.h"
 
 namespace dmlc_amd {
@@ -61,10 +63,11 @@ struct Shared {  // LDS of one workgroup
   uint32_t npass;
 };
 
-DA_HD uint32_t class_of_csv(uint32_t b, uint32_t delim) {
+DA_HD uint32_t class_of_csv(uint32_t b, uint32_t delim, bool blanks) {
   if (b == delim) return 0x01000000u;
   if (is_digitchar(b)) return is_digit(b) ? 0x00000101u : 0x00000001u;
   if (b == '\n' || b == '\r') return 0x00010000u;
+  if (blanks && (b == ' ' || b == '\t')) return 0u;  // blank: class 0
   return 0x00000100u;  // outside the grammar: "digit" without "number char"
 }
 
@@ -160,12 +163,36 @@ struct Tile {
       if (sh->c.csl[i] > p) return sh->c.csl[i];
     return sh->c.cnext;
   }
+  DA_HD bool is_cs(uint64_t p) const {
+    for (uint32_t i = 0; i < sh->c.ncs; ++i)
+      if (sh->c.csl[i] == p) return true;
+    return p == sh->c.cnext;
+  }
 };
+
+// strtoll(p, &e, 0) (csv_parser.h:101-105) on a token of the grammar: [sign]
+// digits, decimal -- a leading 0 followed by a digit is octal and goes to the
+// byte decoder, as do more than 8 digits (saturation); *ok = false then.
+// M: bit i set when window byte i is not '0'..'9' (16 bits)
+DA_HD int64_t wint64m(const uint32_t w[4], uint32_t M, bool *ok) {
+  const uint32_t b0 = w[0] & 0xFFu;
+  const bool neg = b0 == '-';
+  const uint32_t s = (neg || b0 == '+') ? 1u : 0u;
+  const uint32_t L = (uint32_t)ctz32((M & ~s) | 0x10000u) - s;
+  const uint32_t d0 = byte_of(w, s);
+  *ok = L >= 1u && L <= 8u && !(d0 == '0' && L > 1u);
+  if (!*ok) return 0;
+  const int64_t v = (int64_t)digits_ra(w, s, L);
+  return neg ? -v : v;
+}
 
 // MODE 1: count only (size query); MODE 2: parse and write.
 // SP: label / weight columns may be set (a separate kernel, so the plain
-// form carries none of their code)
-template <int MODE, bool SP, class BK>
+// form carries none of their code); blanks are outside its grammar.
+// VT: 0 float values (ParseFloat), 1 integer values (strtoll base 0, int32 /
+// int64 by a.vtype; no label column, the weight column is a plain column for
+// integer DTypes, csv_parser.h:111-114).
+template <int MODE, bool SP, int VT, class BK>
 DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
   // Tile k = workgroup k (its blockIdx).  The look-back needs every tile's
   // predecessors to become resident eventually; workgroups are dispatched in
@@ -191,7 +218,7 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
     sh.u.m.d[0] = sh.u.m.n[0] = sh.u.m.l[0] = 0;
     sh.nlab = sh.nfirst = 0;
   }
-  sh.cls[tid] = class_of_csv((uint32_t)tid, a.delim);
+  sh.cls[tid] = class_of_csv((uint32_t)tid, a.delim, !SP);
   init_dec_tables(sh.dt, bk);
   stage_commit(a.text, a.n, t.tlo, sr, sh.c, bk);
   bk.sync();
@@ -237,17 +264,64 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
   if (P < a.n) {
     const int nv = (int)mn<uint64_t>(64, a.n - P);
     const uint64_t valid = nv == 64 ? ~0ull : ((1ull << nv) - 1);
-    const uint64_t N = sh.u.m.n[tid + 1];
+    const uint64_t N = sh.u.m.n[tid + 1], D = sh.u.m.d[tid + 1];
     L = sh.u.m.l[tid + 1] & valid;
     uint64_t S = 0;  // chunk starts: a "newline before" for the row rule, a field barrier
     for (uint32_t i = 0; i < sh.c.ncs; ++i) {
       const uint64_t x = sh.c.csl[i];
       if (x >= P && x < P + (uint64_t)nv) S |= 1ull << (x - P);
     }
-    const uint64_t nprev = (sh.u.m.n[tid] >> 63) & 1u, lprev = (sh.u.m.l[tid] >> 63) & 1u;
-    RS = ~N & valid & ((N << 1) | nprev | S);
-    const uint64_t FSd = ((L << 1) | lprev) & ~N & ~S & valid;
-    T = (RS | FSd) & sh.u.m.d[tid + 1];
+    const uint64_t n1 = sh.u.m.n[tid], l1 = sh.u.m.l[tid];
+    RS = ~N & valid & ((N << 1) | (n1 >> 63) | S);
+    const uint64_t FSd = ((L << 1) | (l1 >> 63)) & ~N & ~S & valid;
+    const uint64_t F = RS | FSd;  // field starts
+    if constexpr (SP) {
+      T = F & D;
+    } else {
+      // Blanks (' ', '\t', class 0): ParseFloat / strtoll skip them at a field
+      // start (strtonum.h:95-264), so a field's token is the first non-blank
+      // byte after its start -- found by a carry through the blank run that
+      // begins at a blank field start (a field start always begins its run).
+      // The run carried in from the segment before when that one ends in
+      // blanks which follow a delimiter, a newline or a chunk start.
+      const uint64_t B = ~(D | N | L) & valid;
+      uint32_t cin = 0;
+      if (P > 0 && !(S & 1u)) {
+        const uint64_t nb1 = sh.u.m.d[tid] | n1 | l1;  // non-blank bytes of the segment before
+        if (!(nb1 >> 63)) {
+          if (!nb1) {
+            bad = 1;  // 64 blanks in a row: beyond this carry, the exact kernels take it
+          } else {
+            const uint32_t j = 63u - (uint32_t)clz64(nb1);
+            const uint64_t x = P - 64u + j + 1u;  // the run's first byte
+            bool cs = x == sh.c.cfloor;
+            for (uint32_t i = 0; i < sh.c.ncs; ++i) cs = cs || sh.c.csl[i] == x;
+            cin = (((n1 | l1) >> j) & 1u) || cs ? 1u : 0u;
+          }
+        }
+      }
+      uint32_t cout;
+      const uint64_t land = add_carry(B, F & B, cin, &cout) & ~B;  // first non-blank after a blank field start
+      // the run reaches a newline, a chunk start or the text end: ParseFloat /
+      // strtoll would skip on into the next line (csv_parser.h:99-105)
+      if (land & (N | S | ~valid)) bad = 1;
+      if (cout && (P + 64 >= a.n || t.is_cs(P + 64))) bad = 1;
+      if constexpr (VT == 0) {
+        // a blank field ending at a delimiter is ParseFloat's 0 (it consumed the blanks)
+        T = (F & D) | (land & (D | L));
+      } else {
+        // strtoll consumed nothing unless a digit follows the optional sign:
+        // the field is then a missing value (csv_parser.h:115-118)
+        const uint64_t C = (F & D) | (land & D);
+        const uint64_t G = (uint64_t)sh.gw[2 * tid] | ((uint64_t)sh.gw[2 * tid + 1] << 32);
+        const uint64_t Gn = (G >> 1) | ((uint64_t)(sh.gw[2 * tid + 2] & 1u) << 63);  // next byte a digit
+        T = C & G;
+        for (uint64_t m = C & ~G & Gn; m; m &= m - 1) {
+          const uint32_t b = sh.c.text[kPre + tid * kSegB + ctz64(m)];
+          if (b == '-' || b == '+') T |= m & (0 - m);
+        }
+      }
+    }
   }
   if (bad) atomic_or_u32(&sh.c.bad, 1u);
   // segmented delimiter count of my segment: since my last row start, or all
@@ -274,30 +348,46 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
     if (sh.c.bad) atomic_or_u32(a.gate, 1u);
   }
   const bool one_chunk = sh.c.ncs == 0;
-  auto dec_float = [&](uint64_t q) -> float {
+  // the value of the token at q: float (VT 0) or the strtoll result (VT 1)
+  using Val = typename std::conditional<VT == 0, float, int64_t>::type;
+  auto dec_float = [&](uint64_t q) -> Val {
     const uint32_t o = (uint32_t)(q - t.tlo);  // non-digit flags of the window from the digit plane
     const uint32_t M = ~funnel(sh.gw[(o >> 5) + 1], sh.gw[o >> 5], o & 31u);
     const uint64_t lim = one_chunk ? sh.c.cnext : t.next_cs(q);
     bool ok = false;
-    float v = 0.f;
+    Val v = 0;
     if (q + 16 <= lim) {
       const W16 wq = win_at(sh.c.text, t.tlo, q);
       const uint32_t w4[4] = {(uint32_t)wq.lo, (uint32_t)(wq.lo >> 32), (uint32_t)wq.hi, (uint32_t)(wq.hi >> 32)};
-      v = wfloat32m(w4, M, sh.dt, &ok);
+      if constexpr (VT == 0) v = wfloat32m(w4, M, sh.dt, &ok);
+      else v = wint64m(w4, M, &ok);
     }
     if (!ok) {
       GSrc src{a.text, lim};
       uint64_t e;
-      bool nan_err = false;
-      v = parse_float(src, q, &e, &nan_err);
+      if constexpr (VT == 0) {
+        bool nan_err = false;
+        v = parse_float(src, q, &e, &nan_err);
+      } else {
+        v = c_strtoll(src, q, 0, &e);
+      }
     }
     return v;
+  };
+  // the value array: DType float, or int32 / int64 (a.vtype 1 / 2)
+  auto put_val = [&](uint64_t g, Val v) {
+    if constexpr (VT == 0) {
+      reinterpret_cast<float *>(a.value)[g] = v;
+    } else {
+      if (a.vtype == 1) reinterpret_cast<int32_t *>(a.value)[g] = (int32_t)v;
+      else reinterpret_cast<int64_t *>(a.value)[g] = v;
+    }
   };
 #ifndef FCSV_KB
 #define FCSV_KB 4
 #endif
   constexpr int kB = FCSV_KB;  // tokens decoded before the look-back
-  float vb[kB > 0 ? kB : 1];
+  Val vb[kB > 0 ? kB : 1];
   uint64_t mT = T;
   const bool has_lab = SP && a.label_col >= 0, has_w = SP && a.weight_col >= 0;
   const bool has_sp = has_lab || has_w;  // special columns: tokens stored per token, not listed
@@ -342,13 +432,13 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
 #pragma unroll
     for (int u = 0; u < kB; ++u) {
       const uint32_t j = (uint32_t)tid + (uint32_t)u * kThreads;
-      vb[u] = 0.f;
+      vb[u] = 0;
       if (j < pe0) vb[u] = dec_float(t.tlo + (sh.u.lst[j] & 0x3FFFu));
     }
   } else if (MODE == 2) {
 #pragma unroll
     for (int u = 0; u < kB; ++u) {
-      vb[u] = 0.f;
+      vb[u] = 0;
       if (mT) {
         vb[u] = dec_float(P + ctz64(mT));
         mT &= mT - 1;
@@ -427,7 +517,7 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
   if (MODE != 2) return;
 
   // ---- stores: values and column indices (labels), then row offsets
-  auto put = [&](uint64_t g, uint32_t b, float v) {  // g: global token rank
+  auto put = [&](uint64_t g, uint32_t b, Val v) {  // g: global token rank
     const uint64_t c = col_of(b);
     const uint64_t sp_before = (c > Lc ? 1u : 0u) + (c > Wc ? 1u : 0u);
     if (has_sp) {
@@ -447,7 +537,7 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
     }
     const uint64_t ci = c - sp_before;
     if (g < a.cap[C_VALUE] && g < a.cap[C_INDEX]) {
-      a.value[g] = v;
+      put_val(g, v);
       if (a.wide) reinterpret_cast<uint64_t *>(a.index)[g] = ci;
       else reinterpret_cast<uint32_t *>(a.index)[g] = (uint32_t)ci;
     } else {
@@ -456,10 +546,10 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
   };
   if (!has_sp) {
     // list entry j of the pass starting at token s0: value rank bVal + s0 + j
-    auto put_tok = [&](uint64_t g, uint32_t e, float v) {
+    auto put_tok = [&](uint64_t g, uint32_t e, Val v) {
       const uint64_t ci = ((e >> 14) & ((1u << kColBits) - 1)) + ((e >> 31) ? tcarry : 0u);
       if (g < a.cap[C_VALUE] && g < a.cap[C_INDEX]) {
-        a.value[g] = v;
+        put_val(g, v);
         if (a.wide) reinterpret_cast<uint64_t *>(a.index)[g] = ci;
         else reinterpret_cast<uint32_t *>(a.index)[g] = (uint32_t)ci;
       } else {

@@ -354,7 +354,7 @@ DA_HD bool wuint(const W16 &w, bool wide, uint64_t *out, bool *ok) {
 // rate; 64-bit multiplies and the f64 divide sequence are not)
 struct DecTables {
   double p10[16], i10[16];  // 10^k and RN(10^-k)
-  uint32_t inv5[9];         // 5^-k mod 2^32
+  uint64_t hib[9];          // 0x0F in bytes >= k of 8 (k <= 8): the fraction's byte masks
 };
 // The tables as compile-time constants (constant evaluation divides with
 // IEEE round-to-nearest, so i10[k] is the correctly rounded 10^-k); each tile
@@ -367,10 +367,10 @@ constexpr DecTables make_dec_tables() {
     t.i10[k] = 1.0 / p;
     p *= 10.0;
   }
-  uint32_t v = 1;
-  for (int k = 0; k < 9; ++k) {
-    t.inv5[k] = v;
-    v *= 0xCCCCCCCDu;  // 5^-1 mod 2^32
+  for (int k = 0; k <= 8; ++k) {
+    uint64_t m = 0;
+    for (int b = k; b < 8; ++b) m |= 0x0Full << (8 * b);
+    t.hib[k] = m;
   }
   return t;
 }
@@ -382,7 +382,7 @@ DA_HDF void init_dec_tables(DecTables &tb, BK &bk) {
     tb.p10[t] = kDecTables.p10[t];
     tb.i10[t] = kDecTables.i10[t];
   } else if (t < 25) {
-    tb.inv5[t - 16] = kDecTables.inv5[t - 16];
+    tb.hib[t - 16] = kDecTables.hib[t - 16];
   }
 }
 DA_HD uint32_t udot4(uint32_t a, uint32_t b, uint32_t c) {  // sum of the 4 byte products + c
@@ -408,22 +408,27 @@ DA_HD uint32_t byte_of(const uint32_t w[4], uint32_t p) {  // window byte p < 16
 DA_HD uint64_t low_bytes(uint32_t k) {  // mask of the low k bytes, k <= 8
   return k >= 8 ? ~0ull : ((1ull << (8u * k)) - 1ull);
 }
-// the 8 window bytes from byte s (s <= 1) as nibbles, keeping the first L
-DA_HD uint32_t lead8(const uint32_t w[4], uint32_t s, uint32_t L) {
-  const uint32_t lo = funnel(w[1], w[0], 8u * s), hi = funnel(w[2], w[1], 8u * s);
-  const uint64_t m = low_bytes(L) & 0x0F0F0F0F0F0F0F0Full;
-  return dig4(hi & (uint32_t)(m >> 32), dig4(lo & (uint32_t)m, 0u));  // = value * 10^(8-L)
+// value of the L <= 8 decimal digits at window bytes s .. s+L-1 (s <= 1): the
+// 8 bytes from s shifted up so the digits end at byte 7 -- the bytes after
+// them fall off the top, zeros enter below -- then 4 + 4 digits by dot4 (no
+// division by 10^(8-L), no table)
+DA_HD uint32_t digits_ra(const uint32_t w[4], uint32_t s, uint32_t L) {
+  const uint32_t sh = 8u * s;
+  const uint64_t x = ((uint64_t)funnel(w[2], w[1], sh) << 32) | funnel(w[1], w[0], sh);
+  const uint64_t y = L ? x << (64u - 8u * L) : 0ull;
+  return dig4((uint32_t)(y >> 32) & 0x0F0F0F0Fu, dig4((uint32_t)y & 0x0F0F0F0Fu, 0u));
 }
 
 // ParseFloat<float> (strtonum.h:95-264) on a run of the uniform grammar,
-// 32-bit form: integer part (<= 8 digits) left-aligned in 8 nibbles then an
-// exact division by 10^(8-il) (shift + multiply by 5^-k mod 2^32); fraction
-// digits kept in place in the 16-byte window, V = val2 * 10^(16-pe) < 10^15,
-// so V / 10^(16-fs) is the same real number as val2 / 10^fl and its
-// correctly rounded double is the reference's (double)val2/(double)pow10,
-// computed as a Markstein quotient (one multiply, two FMAs, tabulated
-// reciprocal).  *ok = false: exponent, long parts or a number that may
-// continue past the window (caller falls back to the byte decoder).
+// 32-bit form: integer part (<= 8 digits) right-aligned by a shift and
+// converted by dot4 (digits_ra); the fraction digits [fs, pe) -- the window
+// shifted up so byte pe - 1 lands on byte 15, the bytes below the fraction
+// cleared -- give val2 exactly (< 10^15), and val2 / 10^fl, the reference's
+// (double)val2/(double)pow10, is rounded by a Markstein quotient (one
+// multiply, two FMAs, tabulated reciprocal).  The reference's arithmetic is
+// kept: integer part -> f32, f64 fraction -> f32, f32 add.  *ok = false:
+// exponent, long parts or a number that may continue past the window (caller
+// falls back to the byte decoder).
 // M: bit i set when window byte i is not '0'..'9' (16 bits)
 DA_HD float wfloat32m(const uint32_t w[4], uint32_t M, const DecTables &tb, bool *ok) {
   const uint32_t b0 = w[0] & 0xFFu;
@@ -440,15 +445,15 @@ DA_HD float wfloat32m(const uint32_t w[4], uint32_t M, const DecTables &tb, bool
   const uint32_t ce = dot ? byte_of(w, pe) : c;
   const uint32_t il = p - sg;
   if ((ce | 0x20u) == 'e' || il > 8u) return 0.f;
-  const uint32_t iv8 = lead8(w, sg, il);
-  const uint32_t k = 8u - il;
-  const uint32_t iv = (iv8 >> k) * tb.inv5[k];
-  // fraction bytes [fs, pe) (empty without a '.')
-  const uint64_t mlo = (low_bytes(pe) & ~low_bytes(fs)) & 0x0F0F0F0F0F0F0F0Full;
-  const uint64_t mhi = (low_bytes(pe > 8u ? pe - 8u : 0u) & ~low_bytes(fs > 8u ? fs - 8u : 0u)) &
-                       0x0F0F0F0F0F0F0F0Full;
-  const uint32_t fh = dig4(w[1] & (uint32_t)(mlo >> 32), dig4(w[0] & (uint32_t)mlo, 0u));
-  const uint32_t fo = dig4(w[3] & (uint32_t)(mhi >> 32), dig4(w[2] & (uint32_t)mhi, 0u));
+  const uint32_t iv = digits_ra(w, sg, il);
+  // fraction bytes [fs, pe) (empty without a '.', pe < fs): tabulated byte
+  // masks of each 8-byte half
+  const uint32_t fs8 = fs < 8u ? fs : 8u, pe8 = pe < 8u ? pe : 8u;
+  const uint32_t fsh = fs > 8u ? fs - 8u : 0u, peh = pe > 8u ? pe - 8u : 0u;
+  const uint64_t flo = ((uint64_t)w[1] << 32 | w[0]) & tb.hib[fs8] & ~tb.hib[pe8];
+  const uint64_t fhi = ((uint64_t)w[3] << 32 | w[2]) & tb.hib[fsh] & ~tb.hib[peh];
+  const uint32_t fh = dig4((uint32_t)(flo >> 32), dig4((uint32_t)flo, 0u));
+  const uint32_t fo = dig4((uint32_t)(fhi >> 32), dig4((uint32_t)fhi, 0u));
   const double v = __builtin_fma((double)fh, 1e8, (double)fo);  // exact: < 10^15
   const uint32_t e = 16u - fs;                                  // 1..15
   const double r = tb.i10[e], t = v * r;
@@ -476,8 +481,7 @@ DA_HD bool wuint32m(const uint32_t w[4], uint32_t M, const DecTables &tb, uint64
     *ok = false;
     return true;
   }
-  const uint32_t k = 8u - L;
-  *out = (lead8(w, s, L) >> k) * tb.inv5[k];
+  *out = digits_ra(w, s, L);
   return true;
 }
 DA_HD bool wuint32(const uint32_t w[4], const DecTables &tb, uint64_t *out, bool *ok) {

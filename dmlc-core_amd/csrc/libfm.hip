@@ -69,6 +69,9 @@ hipError_t launch_libfm(const LibfmArgs &a, const FastSvmArgs &f, bool use_fast,
     if (phase == kPhaseCount) {
       fm_fast_tile<1><<<f.ntiles, kThreads, 0, s>>>(f);
     } else {
+      if (f.indexing_mode < 0 &&
+          (e = hipMemsetAsync(f.umin, 0xFF, (size_t)f.nchunk * sizeof(uint64_t), s)) != hipSuccess)
+        return e;
       prof_mark(0, s, "fm_fast_tile<2>");
       fm_fast_tile<2><<<f.ntiles, kThreads, 0, s>>>(f);
       prof_mark(1, s, "fm_fast_tile<2>");
@@ -112,6 +115,10 @@ hipError_t launch_libfm(const LibfmArgs &a, const FastSvmArgs &f, bool use_fast,
   }
   fm_select_kernel<<<1, 1, 0, s>>>(res, gate, f.err);
   if (phase != kPhaseCount && a.chunk_tab && a.nchunk > 0) chunk_fixup_kernel<<<1, 256, 0, s>>>(a.chunk_tab, a.nchunk, res);
+  if (use_fast && phase != kPhaseCount && f.indexing_mode < 0 &&
+      (e = launch_umin_fix(f.index, f.field, f.wide, f.chunk_tab, f.nchunk, f.umin, res, gate, f.cap[C_INDEX], s)) !=
+          hipSuccess)
+    return e;
   return hipGetLastError();
 }
 

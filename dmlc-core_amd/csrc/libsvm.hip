@@ -22,6 +22,11 @@ __global__ void __launch_bounds__(kThreads) libsvm_tile(LibsvmArgs a) {
   svm::tile<MODE>(a, sh, bk, blockIdx.x);
 }
 
+// LDS is allocated in 512-byte granules: 6 workgroups per CU need <= 53 of
+// them (160 KiB / 6 = 27306 B), one byte more and the launch drops to 5
+static_assert(sizeof(fsvm::Shared) + kBlockScratchU64 * 8 <= 53 * 512,
+              "svm_fast_tile LDS above the 6-workgroup budget");
+
 template <int MODE>
 #ifndef FSVM_MINW
 #define FSVM_MINW 6  // workgroups per CU the fill kernel is register-budgeted for
@@ -99,6 +104,9 @@ hipError_t launch_libsvm(const LibsvmArgs &a, const FastSvmArgs &f, bool use_fas
       svm_fast_tile<1><<<f.ntiles, kThreads, 0, s>>>(f);
       prof_mark(1, s, "svm_fast_tile<1>");
     } else {
+      if (f.indexing_mode < 0 &&
+          (e = hipMemsetAsync(f.umin, 0xFF, (size_t)f.nchunk * sizeof(uint64_t), s)) != hipSuccess)
+        return e;
       prof_mark(0, s, "svm_fast_tile<2>");
       svm_fast_tile<2><<<f.ntiles, kThreads, 0, s>>>(f);
       prof_mark(1, s, "svm_fast_tile<2>");
@@ -143,6 +151,10 @@ hipError_t launch_libsvm(const LibsvmArgs &a, const FastSvmArgs &f, bool use_fas
   }
   select_kernel<<<1, 1, 0, s>>>(res, gate, f.err);
   if (phase != kPhaseCount && f.chunk_tab && f.nchunk > 0) chunk_fixup_kernel<<<1, 256, 0, s>>>(f.chunk_tab, f.nchunk, res);
+  if (use_fast && phase != kPhaseCount && f.indexing_mode < 0 &&
+      (e = launch_umin_fix(f.index, nullptr, f.wide, f.chunk_tab, f.nchunk, f.umin, res, gate, f.cap[C_INDEX], s)) !=
+          hipSuccess)
+    return e;
   return hipGetLastError();
 }
 

@@ -46,6 +46,44 @@ DA_HD bool qid_decide(uint64_t total, uint64_t *res, uint32_t *gate) {
   return true;
 }
 
+// ---- indexing_mode < 0 (libsvm_parser.h:165-171; libfm_parser.h:133-143)
+// on the single-pass path: the write pass stores the ids as read and notes
+// each ParseBlock unit's minimum stored id (umin, libfm: over fields and
+// indices); afterwards every id of a unit holding ids, all of them > 0, drops
+// by one.  The units' index ranges are the chunk table's index column (tab,
+// nunit rows of 8, complete after chunk_fixup_kernel).  Entries [lo, hi) of
+// the index array (and the field array, when set), stride `step` from lo.
+DA_HD int unit_of_entry(const uint64_t *tab, int nunit, uint64_t i) {  // last unit whose range starts <= i
+  int lo = 0, hi = nunit;
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (tab[(uint64_t)mid * 8 + C_INDEX] <= i) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+DA_HD void umin_fix(void *index, void *field, int wide, const uint64_t *tab, int nunit, const uint64_t *umin,
+                    uint64_t total, uint64_t lo, uint64_t hi, uint64_t first, uint64_t step) {
+  if (lo >= hi || nunit < 1) return;
+  for (int u = unit_of_entry(tab, nunit, lo); u < nunit; ++u) {
+    const uint64_t ulo = tab[(uint64_t)u * 8 + C_INDEX];
+    if (ulo >= hi) break;
+    const uint64_t uhi = u + 1 < nunit ? tab[(uint64_t)(u + 1) * 8 + C_INDEX] : total;
+    const uint64_t m = umin[u];
+    if (m == ~0ull || m == 0) continue;  // no ids, or a 0 among them: kept
+    const uint64_t a = ulo > lo ? ulo : lo, b = uhi < hi ? uhi : hi;
+    for (uint64_t i = a + first; i < b; i += step) {
+      if (wide) {
+        --reinterpret_cast<uint64_t *>(index)[i];
+        if (field) --reinterpret_cast<uint64_t *>(field)[i];
+      } else {
+        --reinterpret_cast<uint32_t *>(index)[i];
+        if (field) --reinterpret_cast<uint32_t *>(field)[i];
+      }
+    }
+  }
+}
+
 // ---- "qid:<n>" (libsvm_parser.h:119-132) in the fast grammar.  The letters
 // q, i, d classify as N and C together (fast_common.h class_of); qid_clean
 // makes them blanks and the token's ':' a qid marker (N and C together), so
@@ -892,7 +930,11 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
   const uint64_t mine = (uint64_t)popc64(so.L) | ((uint64_t)popc64(so.W) << 16) |
                         ((uint64_t)popc64(so.I) << 32) | ((uint64_t)popc64(so.V) << 48);
   uint64_t totp;
+#ifdef FSVM_DPP_SCAN
+  const uint64_t ex = bk.exclusive_add(mine, &totp);
+#else
   const uint64_t ex = bk.exclusive(mine, (uint64_t)0, AddU64(), &totp);
+#endif
   FAST_STAMP(k, 4);
   const uint32_t nL = (uint32_t)(totp & 0xFFFF), nW = (uint32_t)((totp >> 16) & 0xFFFF),
                  nI = (uint32_t)((totp >> 32) & 0xFFFF), nV = (uint32_t)(totp >> 48);
@@ -1090,7 +1132,22 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
 
   // ---- stores
   const uint64_t eL = bRows + fL(ex), eW = bW + fW(ex), eI = bIdx + fI(ex), eV = bVal + fV(ex);
+  // indexing_mode < 0: the minimum stored id of each unit (umin_fix): in a
+  // register when the tile lies inside one unit, else a device atomic per id
+  const bool imin = a.indexing_mode < 0;
+  uint64_t tmin = ~0ull;
+  auto note_min = [&](uint64_t q, uint64_t v) {
+    const uint64_t sv = a.wide ? v : (uint64_t)(uint32_t)v;
+    if (one_chunk) {
+      tmin = sv < tmin ? sv : tmin;
+    } else {
+      uint32_t u = sh.c.c_first - 1;
+      for (uint32_t i = 0; i < sh.c.ncs; ++i) u += sh.c.csl[i] <= q ? 1u : 0u;
+      atomic_min_u64((unsigned long long *)&a.umin[u], (unsigned long long)sv);
+    }
+  };
   auto put_index = [&](uint64_t r, uint64_t v, uint64_t q) {
+    if (imin) note_min(q, v);
 #ifdef FSVM_ABL_NOSTORE  // timing ablation only
     if (v == 0x123456789ull) a.res[15] = r;
     return;
@@ -1140,6 +1197,7 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
     if (!ok) pos = slow_uint(a.text, q, lim, a.wide, &v);
     if (!pos) v = 0;
     if (a.indexing_mode > 0) --v;
+    if (imin) note_min(q, v);
     if (r < a.cap[C_FIELD]) {
       if (a.wide) reinterpret_cast<uint64_t *>(a.field)[r] = v;
       else reinterpret_cast<uint32_t *>(a.field)[r] = (uint32_t)v;
@@ -1204,6 +1262,16 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
       if (sh.c.text[q - t.tlo + kPre] == '-') raise_error(a.err, E_NEG_INDEX, q);
     }
   }
+  if (imin && one_chunk) {  // block-uniform: one atomic per wave for the tile's unit
+    uint64_t m = tmin;
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+      const uint64_t o = bk.shfl(m, (int)((uint32_t)(tid ^ d) & (kWave - 1)));
+      m = o < m ? o : m;
+    }
+    if ((tid & (kWave - 1)) == 0 && m != ~0ull)
+      atomic_min_u64((unsigned long long *)&a.umin[sh.c.c_first - 1], (unsigned long long)m);
+  }
   FAST_STAMP(k, 8);
   // ---- per-chunk exclusive counts at each chunk start in my segment
   if (a.chunk_tab) {
@@ -1225,4 +1293,37 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
 }
 
 }  // namespace fsvm
+
+#if defined(__HIPCC__)
+namespace {  // one private copy per kernel translation unit (no RDC)
+// indexing_mode < 0 after the single-pass write pass (fsvm::umin_fix); every
+// block first checks whether any unit needs the shift, so 0-based input (a 0
+// id in every unit) costs one small read per block.
+__global__ void __launch_bounds__(256) umin_fix_kernel(void *index, void *field, int wide, const uint64_t *tab,
+                                                       int nunit, const uint64_t *umin, const uint64_t *res,
+                                                       const uint32_t *gate) {
+  if (*gate) return;  // the exact kernels made this result (and applied the rule themselves)
+  __shared__ int need;
+  if (threadIdx.x == 0) need = 0;
+  __syncthreads();
+  for (int u = threadIdx.x; u < nunit; u += 256)
+    if (umin[u] != ~0ull && umin[u] > 0) need = 1;
+  __syncthreads();
+  if (!need) return;
+  const uint64_t total = res[C_INDEX];
+  for (uint64_t b = (uint64_t)blockIdx.x * 4096; b < total; b += (uint64_t)gridDim.x * 4096)
+    fsvm::umin_fix(index, field, wide, tab, nunit, umin, total, b, b + 4096 < total ? b + 4096 : total,
+                   threadIdx.x, 256);
+}
+inline hipError_t launch_umin_fix(void *index, void *field, int wide, const uint64_t *tab, int nunit,
+                                  const uint64_t *umin, const uint64_t *res, const uint32_t *gate,
+                                  uint64_t cap_index, hipStream_t s) {
+  if (nunit < 1 || !tab) return hipSuccess;
+  uint64_t blocks = (cap_index + 4095) / 4096;
+  blocks = blocks < 1 ? 1 : (blocks > 2048 ? 2048 : blocks);
+  umin_fix_kernel<<<(unsigned)blocks, 256, 0, s>>>(index, field, wide, tab, nunit, umin, res, gate);
+  return hipGetLastError();
+}
+}  // namespace
+#endif
 }  // namespace dmlc_amd

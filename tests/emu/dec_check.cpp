@@ -46,7 +46,7 @@ int main(int argc, char **argv) {
   const long n = argc > 1 ? atol(argv[1]) : 1000000;
   st ^= argc > 2 ? (uint64_t)atoll(argv[2]) * 0x9E3779B97F4A7C15ull : 0;
   DecTables tb;
-  for (int t = 0; t < 32; ++t) {
+  for (int t = 0; t < 256; ++t) {
     Blk b{t};
     init_dec_tables(tb, b);
   }

@@ -94,6 +94,12 @@ struct HostBlock {
     sync();
     return r;
   }
+  uint64_t exclusive_add(uint64_t v, uint64_t *total) {  // DevBlock::exclusive_add (packed counters)
+    struct Add {
+      uint64_t operator()(uint64_t a, uint64_t b) const { return a + b; }
+    };
+    return exclusive(v, (uint64_t)0, Add(), total);
+  }
   template <typename T, typename Op>
   T exclusive(T v, T identity, Op op, T *total) {
     static_assert(sizeof(T) <= 64, "scan element");
@@ -193,8 +199,12 @@ extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *c
     // uniform-grammar kernel first, the exact tile kernels when it sets the
     // gate (or indexing_mode < 0 / FLAG_EXACT)
     const bool fm = prm->format == DMLC_AMD_LIBFM;
-    const bool use_fast = nbytes > 0 && prm->indexing_mode >= 0 && !(prm->flags & DMLC_AMD_FLAG_EXACT);
+    const bool use_fast = nbytes > 0 && !(prm->flags & DMLC_AMD_FLAG_EXACT);
     const uint64_t nft = (nbytes + fsvm::kTile - 1) / fsvm::kTile;
+    const bool imin = prm->indexing_mode < 0;
+    std::vector<uint64_t> umin(nchunks > 0 ? nchunks : 1, ~0ull);
+    uint64_t *ftab = chunk_table ? chunk_table : (imin ? sink.data() : nullptr);  // capi.cpp f.chunk_tab
+    if (!count_only && ftab != chunk_table) chunk_prefill(ftab, nchunks);
     uint32_t gate = use_fast ? 0u : 1u;
     unsigned long long ferr = ~0ull;
     std::vector<uint64_t> lb(nft * 8 + 1, 0), qsum(kLabShards * 8, 0);
@@ -241,7 +251,8 @@ extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *c
       f.field = fm ? out->field : nullptr;
       f.value = a.value;
       for (int i = 0; i < 8; ++i) f.cap[i] = out->cap[i];
-      f.chunk_tab = chunk_table;
+      f.chunk_tab = ftab;
+      f.umin = umin.data();
       f.lb = lb.data();
       f.qsum = qsum.data();
       f.gate = &gate;
@@ -294,6 +305,11 @@ extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *c
         }
     } else {
       res[8] = ferr;
+      if (imin && !count_only && ftab) {  // chunk_fixup_kernel, then umin_fix_kernel (svm_fast.h)
+        chunk_fixup(ftab, nchunks, res);
+        fsvm::umin_fix(a.index, fm ? out->field : nullptr, a.wide, ftab, nchunks, umin.data(), res[C_INDEX], 0,
+                       res[C_INDEX], 0, 1);
+      }
     }
     std::fprintf(stderr, "emu: %s path=%s\n", fm ? "libfm" : "libsvm", gate ? "exact" : "fast");
   } else if (prm->format == DMLC_AMD_CSV) {
@@ -329,9 +345,9 @@ extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *c
     a.err = err;
     // mirrors launch_csv (csv.hip): uniform-grammar kernel first, exact tile
     // kernels when it sets the gate (or the parameters are outside its form)
-    const bool use_fast = nbytes > 0 && prm->value_type == DMLC_AMD_F32 &&
-                          csv_fast_columns_ok(prm->label_column, prm->weight_column) &&
-                          a.fast_delim && !(prm->flags & DMLC_AMD_FLAG_EXACT);
+    const bool cols_ok = prm->value_type == DMLC_AMD_F32 ? csv_fast_columns_ok(prm->label_column, prm->weight_column)
+                                                         : csv_fast_int_ok(prm->label_column);
+    const bool use_fast = nbytes > 0 && cols_ok && a.fast_delim && !(prm->flags & DMLC_AMD_FLAG_EXACT);
     uint32_t gate = use_fast ? 0u : 1u;
     std::vector<uint64_t> labsum_v(kLabShards * 8, 0);
     uint64_t *labsum = labsum_v.data();
@@ -349,13 +365,14 @@ extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *c
       f.wide = a.wide;
       f.delim = a.delim;
       f.label_col = prm->label_column;
-      f.weight_col = prm->weight_column;
+      f.weight_col = prm->value_type == DMLC_AMD_F32 ? prm->weight_column : -1;
+      f.vtype = prm->value_type;
       f.label = reinterpret_cast<float *>(out->label);
       f.weight = out->weight;
       f.labsum = labsum;
       f.offset = out->offset;
       f.index = out->index;
-      f.value = reinterpret_cast<float *>(out->value);
+      f.value = out->value;
       for (int i = 0; i < 8; ++i) f.cap[i] = out->cap[i];
       f.chunk_tab = chunk_table;
       f.lb = lb.data();
@@ -365,11 +382,13 @@ extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *c
       for (uint64_t k = 0; k < nft; ++k) {
         fcsv::Shared *sh = new fcsv::Shared;
         std::memset(sh, 0xCD, sizeof(*sh));
-        const bool sp = f.label_col >= 0 || f.weight_col >= 0;
-        if (count_only && sp) run_block([&](HostBlock &bk) { fcsv::tile<1, true>(f, *sh, bk, (uint32_t)k); });
-        else if (count_only) run_block([&](HostBlock &bk) { fcsv::tile<1, false>(f, *sh, bk, (uint32_t)k); });
-        else if (sp) run_block([&](HostBlock &bk) { fcsv::tile<2, true>(f, *sh, bk, (uint32_t)k); });
-        else run_block([&](HostBlock &bk) { fcsv::tile<2, false>(f, *sh, bk, (uint32_t)k); });
+        const bool sp = f.label_col >= 0 || f.weight_col >= 0, iv = f.vtype != 0;
+        if (count_only && iv) run_block([&](HostBlock &bk) { fcsv::tile<1, false, 1>(f, *sh, bk, (uint32_t)k); });
+        else if (iv) run_block([&](HostBlock &bk) { fcsv::tile<2, false, 1>(f, *sh, bk, (uint32_t)k); });
+        else if (count_only && sp) run_block([&](HostBlock &bk) { fcsv::tile<1, true, 0>(f, *sh, bk, (uint32_t)k); });
+        else if (count_only) run_block([&](HostBlock &bk) { fcsv::tile<1, false, 0>(f, *sh, bk, (uint32_t)k); });
+        else if (sp) run_block([&](HostBlock &bk) { fcsv::tile<2, true, 0>(f, *sh, bk, (uint32_t)k); });
+        else run_block([&](HostBlock &bk) { fcsv::tile<2, false, 0>(f, *sh, bk, (uint32_t)k); });
         delete sh;
       }
       if (f.label_col >= 0 || f.weight_col >= 0) {  // label_check_kernel

@@ -323,3 +323,46 @@ def uniform_libfm(rng, nlines, maxtrip=20, violate=False):
     ends = ["\n"] * 10 + ["\r\n", "\n\n"]
     text = "".join(l + ends[int(rng.integers(0, len(ends)))] for l in lines)
     return text.encode()
+
+
+_INTS = ["0", "7", "-3", "+12", "007", "019", "08", "-0", "2147483648", "-2147483649", "99999999",
+         "123456789", "9223372036854775808", "-9223372036854775809", "1e5", "2.5", "-.5", ".5", "+", "-",
+         "e", "00", "0.0", "-0.123"]
+
+
+def blank_csv(rng, nlines, maxcols=30, delim=",", ints=False, violate=False):
+    """CSV with blanks around the values (", " separators, padded and
+    blank-only fields): ParseFloat / strtoll skip the blanks before a value
+    and the reference skips anything after it up to the delimiter
+    (csv_parser.h:99-127).  ints=True draws integer-looking fields (octal,
+    overflow, signs, fractions).  violate=True adds a blank-only last field (the
+    decoder would read on into the next line: the exact kernels)."""
+    out = []
+    for _ in range(nlines):
+        if rng.random() < 0.03:
+            out.append(" " * int(rng.integers(0, 3)) if violate else "")
+            continue
+        fields = []
+        for _ in range(int(rng.integers(1, maxcols + 1))):
+            r = rng.random()
+            if r < 0.06:
+                v = ""
+            elif r < 0.12:
+                v = " " * int(rng.integers(1, 4))  # blank-only field
+            elif ints:
+                v = _INTS[int(rng.integers(0, len(_INTS)))] if rng.random() < 0.4 else str(int(rng.integers(-10 ** 6, 10 ** 6)))
+            else:
+                v = _csv_field(rng)
+            if v.strip():
+                v = " " * int(rng.integers(0, 3) if rng.random() < 0.7 else 0) + v
+                if rng.random() < 0.2:
+                    v += rng.choice([" ", "  ", "\t", " 9"])
+            fields.append(v)
+        if not fields[-1].strip() and not violate:
+            fields[-1] = ""  # a blank-only last field reads on into the next line
+        line = delim.join(fields)
+        if violate and rng.random() < 0.15:
+            line += delim + " "
+        out.append(line)
+    seps = ["\n"] * 10 + ["\r\n", "\n\n"]
+    return "".join(line + seps[int(rng.integers(0, len(seps)))] for line in out).encode("latin-1")

@@ -440,3 +440,79 @@ def test_emu_csv_fast_weight_column():
             assert h["path"] == "fast", (it, lc, wc)
         fast += h["path"] == "fast"
     assert fast >= 10
+
+
+def _one_based(rng, nlines, width, shift_rows=()):
+    """libsvm rows with ids starting at 1 except for the rows in shift_rows,
+    which hold a 0 id (a 0-based unit wherever they land)."""
+    out = []
+    for r in range(nlines):
+        ids = sorted(set(int(x) for x in rng.integers(1, 4000, size=int(rng.integers(1, width)))))
+        if r in shift_rows:
+            ids = [0] + ids
+        out.append("%d %s" % (r % 2, " ".join("%d:%.7g" % (i, rng.random()) for i in ids)))
+    return ("\n".join(out) + "\n").encode()
+
+
+@pytest.mark.parametrize("nthread", [1, 3])
+def test_emu_fast_indexing_mode_auto(nthread):
+    """indexing_mode=-1 on the single-pass path (libsvm_parser.h:165-171):
+    per ParseBlock unit (chunk x FillData range) the ids drop by one when the
+    unit holds ids, all > 0; units with a 0 id keep theirs.  1-based and
+    0-based units side by side, multi-tile, both id widths."""
+    rng = np.random.default_rng(5150 + nthread)
+    for it in range(4):
+        n = 400 if it < 2 else 40
+        data = _one_based(rng, n, 50 if it < 2 else 8, shift_rows=set(rng.integers(0, n, size=it).tolist()))
+        offs = fuzz_text.random_cuts(rng, data, 6)
+        kw = {"indexing_mode": -1, "nthread": nthread, "index_bits": 64 if it % 2 else 32}
+        h = _emu_vs_oracle(data, offs, **kw)
+        assert h["path"] == "fast", it
+
+
+def test_emu_fast_libfm_indexing_mode_auto():
+    rng = np.random.default_rng(616)
+    for it in range(3):
+        rows = []
+        for r in range(200):
+            k = int(rng.integers(1, 12))
+            lo = 0 if (it == 1 and r == 77) else 1
+            rows.append("%d %s" % (r % 2, " ".join("%d:%d:%.6g" % (int(rng.integers(lo, 9)), int(rng.integers(lo, 500)),
+                                                                     rng.random()) for _ in range(k))))
+        data = ("\n".join(rows) + "\n").encode()
+        offs = fuzz_text.random_cuts(rng, data, 4)
+        o = po.parse_chunks(data, offs, fmt=po.LIBFM, indexing_mode=-1)
+        h = pyemu.parse(data, offs, "libfm", indexing_mode=-1)
+        assert h["error"] == 0 and o["status"] == 0 and h["path"] == "fast"
+        assert diff(h, o) == [], diff(h, o)
+
+
+@pytest.mark.parametrize("vt", ["f32", "i32", "i64"])
+def test_emu_csv_fast_blanks_and_ints(vt):
+    """Blanks around CSV values and integer DTypes on the single-pass CSV
+    kernel (csv_fast.h): the token of a field is its first non-blank byte; a
+    blank-only field is ParseFloat's 0 but strtoll's missing value; integer
+    tokens need a digit after the sign (strtoll base 0: octal, saturation by
+    the byte decoder).  Multi-tile and odd chunkings; violations (a blank
+    field running into the next line) go to the exact kernels."""
+    rng = np.random.default_rng({"f32": 31, "i32": 32, "i64": 33}[vt])
+    paths = {"fast": 0, "exact": 0}
+    vmap = {"f32": 0, "i32": 1, "i64": 2}
+    for it in range(24):
+        big = it % 6 == 5
+        violate = (not big) and rng.random() < 0.3
+        data = fuzz_text.blank_csv(rng, 1500 if big else int(rng.integers(1, 40)), 40 if big else 20,
+                                   ints=vt != "f32" or rng.random() < 0.2, violate=violate)
+        offs = fuzz_text.random_cuts(rng, data, 5)
+        kw = {"value_type": vmap[vt]}
+        if vt != "f32" and rng.random() < 0.3:
+            kw["weight_column"] = int(rng.integers(0, 3))  # an ordinary column for integer DTypes
+        okw = {("value_kind" if k == "value_type" else k): v for k, v in kw.items()}
+        o = po.parse_chunks(data, offs, fmt=po.CSV, **okw)
+        h = pyemu.parse(data, offs, "csv", **kw)
+        failed = check_fail(h, "csv", offs)
+        assert (o["status"] != 0) == failed, (it, data[:300], offs, o["msg"], h["error"])
+        if not failed:
+            assert diff(h, o) == [], (it, diff(h, o), data[:300])
+        paths[h["path"]] += 1
+    assert paths["fast"] >= 12, paths

@@ -823,3 +823,102 @@ def test_gpu_qid_letter_forms_vs_oracle(dm, fmt):
     for line in lines:
         for data in (line, "0 1:1\n" * 7000 + line + "0 1:1\n" * 3000):
             _gpu_vs_oracle_paths(dm, data, [0, len(data)], fmt=fmt)
+
+
+def _gpu_vs_oracle_vt(dm, data, offs, vt, **kw):
+    """_gpu_vs_oracle_paths with a CSV value type (the oracle calls it value_kind)."""
+    o = po.parse_chunks(data, offs, fmt=po.CSV, value_kind=vt, **kw)
+    res = {}
+    for exact in (False, True):
+        h = dm.parse_bytes(data, offs, fmt="csv", exact=exact, value_type=vt, **kw)
+        nch = len(offs) - 1
+        failed = bool(h["error"]) or (nch > 0 and dm.chunk_check(h, "csv", nch, h["counts"]) >= 0)
+        assert (o["status"] != 0) == failed, (exact, o["msg"], h["error"], data[:200], offs, kw)
+        if not failed:
+            assert diff(h, o) == [], (exact, diff(h, o), offs, kw)
+        res[exact] = h
+    if o["status"] == 0:
+        assert res[False]["chunk_table"].tolist() == res[True]["chunk_table"].tolist()
+    return res[False]
+
+
+@pytest.mark.parametrize("vt", [0, 1, 2])
+def test_gpu_csv_fast_blanks_and_ints_vs_oracle(dm, vt):
+    """Blanks around values (", " separators, padded and blank-only fields)
+    and integer DTypes (strtoll base 0) on the single-pass CSV kernels
+    (csv_fast.h): bit-exact against the oracle on both paths, most inputs on
+    the single pass; a blank field that runs into the next line goes exact."""
+    rng = np.random.default_rng(900 + vt)
+    paths = {"fast": 0, "exact": 0}
+    for it in range(120):
+        big = it % 10 == 9
+        delim = ",;|"[it % 3]
+        data = fuzz_text.blank_csv(rng, 2500 if big else int(rng.integers(1, 40)), 50 if big else 25, delim,
+                                   ints=vt != 0 or rng.random() < 0.2, violate=(not big) and rng.random() < 0.2)
+        offs = fuzz_text.random_cuts(rng, data, 8 if big else 5, anywhere=rng.random() < 0.2)
+        kw = {"delimiter": delim}
+        if rng.random() < 0.2:
+            kw["index_bits"] = 64
+        if vt and rng.random() < 0.3:
+            kw["weight_column"] = int(rng.integers(0, 3))
+        try:
+            paths[_gpu_vs_oracle_vt(dm, data, offs, vt, **kw)["path"]] += 1
+        except AssertionError as e:
+            raise AssertionError("case %d: %s" % (it, e))
+    assert paths["fast"] > 70, paths
+
+
+def test_gpu_csv_variant_bench_configs_fast(dm):
+    """The bench's CSV grammar variants (", " separators; int32 DType) run on
+    the single-pass kernels and equal the exact kernels bit for bit at 100k
+    rows x 256 columns."""
+    import torch
+    for fmt, vt in ((synth.CSV_SP, 0), (synth.CSV, 1), (synth.CSV_SP, 2)):
+        text, _ = synth.rows(fmt, 100000, 256, seed=3)
+        starts = dm.text_chunk_starts(text)
+        d_text = torch.from_numpy(text).cuda()
+        d_cs = torch.from_numpy(starts).cuda()
+        outs = {}
+        for exact in (False, True):
+            p = dm.DeviceParser("csv", value_type=vt, flags=dm.FLAG_EXACT if exact else 0)
+            out = p.parse(d_text, d_cs)
+            assert out["error"] == 0 and out["path"] == (1 if exact else 0), (fmt, vt, exact, out["path"])
+            outs[exact] = out
+        assert outs[False]["counts"][:7] == outs[True]["counts"][:7]
+        for k in ("offset", "index", "value"):
+            assert torch.equal(outs[False][k], outs[True][k]), (fmt, vt, k)
+
+
+@pytest.mark.parametrize("nthread", [1, 2])
+def test_gpu_fast_indexing_mode_auto_vs_oracle(dm, nthread):
+    """indexing_mode=-1 on the single-pass libsvm / libfm kernels: each
+    ParseBlock unit's ids drop by one when all of them are > 0
+    (libsvm_parser.h:165-171, libfm_parser.h:133-143); 1-based and 0-based
+    units side by side, tile-crossing unit starts, both id widths."""
+    rng = np.random.default_rng(64 + nthread)
+    for it in range(12):
+        rows = []
+        n = int(rng.integers(50, 3000))
+        zeros = set(rng.integers(0, n, size=int(rng.integers(0, 3))).tolist())
+        for r in range(n):
+            ids = sorted(set(int(x) for x in rng.integers(1, 100000, size=int(rng.integers(1, 40)))))
+            if r in zeros:
+                ids = [0] + ids
+            rows.append("%d %s" % (r % 2, " ".join("%d:%.7g" % (i, rng.random()) for i in ids)))
+        data = ("\n".join(rows) + "\n").encode()
+        offs = fuzz_text.random_cuts(rng, data, 8)
+        kw = {"indexing_mode": -1, "nthread": nthread, "index_bits": 64 if it % 3 == 2 else 32}
+        h = _gpu_vs_oracle_paths(dm, data, offs, **kw)
+        assert h["path"] == "fast", it
+    # libfm
+    rng = np.random.default_rng(99)
+    for it in range(6):
+        rows = []
+        for r in range(1500):
+            lo = 0 if (it % 2 and r == 700) else 1
+            rows.append("%d %s" % (r % 2, " ".join("%d:%d:%.6g" % (int(rng.integers(lo, 9)), int(rng.integers(lo, 900)),
+                                                                     rng.random()) for _ in range(int(rng.integers(1, 12))))))
+        data = ("\n".join(rows) + "\n").encode()
+        offs = fuzz_text.random_cuts(rng, data, 5)
+        h = _gpu_vs_oracle_paths(dm, data, offs, fmt=po.LIBFM, indexing_mode=-1, nthread=nthread)
+        assert h["path"] == "fast", it
