@@ -5,8 +5,14 @@
 
 namespace dmlc_amd {
 
-struct DevBlock {
-  // LDS scratch: (kWaves + 1) slots of up to 64 bytes
+// kSlot: bytes per scan slot in the LDS scratch -- the largest scan element
+// the kernel uses (64 for the counter vectors of the exact kernels, 8 for the
+// single-pass kernels, whose LDS budget is tight: fast_common.h kLdsBudget)
+template <int kSlot>
+struct DevBlockT {
+  static_assert(kSlot % 8 == 0 && kSlot >= 8, "8-byte granular slots");
+  static constexpr int kSlotU64 = kSlot / 8;
+  // LDS scratch: (kWaves + 1) slots of kSlot bytes
   uint64_t *scratch;
 
   __device__ __forceinline__ int tid() const { return threadIdx.x; }
@@ -57,11 +63,11 @@ struct DevBlock {
       const uint64_t o = __shfl_xor(v, d, kWave);
       v = o < v ? o : v;
     }
-    if (lane == 0) scratch[wid * 8] = v;
+    if (lane == 0) scratch[wid * kSlotU64] = v;
     __syncthreads();
     uint64_t r = scratch[0];
 #pragma unroll
-    for (int w = 1; w < kWaves; ++w) r = scratch[w * 8] < r ? scratch[w * 8] : r;
+    for (int w = 1; w < kWaves; ++w) r = scratch[w * kSlotU64] < r ? scratch[w * kSlotU64] : r;
     __syncthreads();
     return r;
   }
@@ -101,7 +107,7 @@ struct DevBlock {
   // Exclusive prefix (identity for thread 0) and the block total.
   template <typename T, typename Op>
   __device__ __forceinline__ T exclusive(T v, T identity, Op op, T *total) const {
-    static_assert(sizeof(T) <= 64, "scan element too large");
+    static_assert(sizeof(T) <= kSlot, "scan element larger than the scratch slot");
     T *sc = reinterpret_cast<T *>(scratch);
     const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
     T inc = v;
@@ -110,31 +116,35 @@ struct DevBlock {
       T o = shfl_up(inc, d);
       if (lane >= d) inc = op(o, inc);
     }
-    T *slot = reinterpret_cast<T *>(reinterpret_cast<char *>(sc) + 64 * wid);
+    T *slot = reinterpret_cast<T *>(reinterpret_cast<char *>(sc) + kSlot * wid);
     if (lane == kWave - 1) *slot = inc;
     __syncthreads();
     if (threadIdx.x == 0) {
       T acc = *reinterpret_cast<T *>(reinterpret_cast<char *>(sc));
       for (int w = 1; w < kWaves; ++w) {
-        T *sw = reinterpret_cast<T *>(reinterpret_cast<char *>(sc) + 64 * w);
+        T *sw = reinterpret_cast<T *>(reinterpret_cast<char *>(sc) + kSlot * w);
         T t = *sw;
         *sw = acc;
         acc = op(acc, t);
       }
       *reinterpret_cast<T *>(reinterpret_cast<char *>(sc)) = identity;
-      *reinterpret_cast<T *>(reinterpret_cast<char *>(sc) + 64 * kWaves) = acc;
+      *reinterpret_cast<T *>(reinterpret_cast<char *>(sc) + kSlot * kWaves) = acc;
     }
     __syncthreads();
     const T up = shfl_up(inc, 1);
-    const T wpre = *reinterpret_cast<T *>(reinterpret_cast<char *>(sc) + 64 * wid);
+    const T wpre = *reinterpret_cast<T *>(reinterpret_cast<char *>(sc) + kSlot * wid);
     const T ex = lane == 0 ? wpre : op(wpre, up);
-    *total = *reinterpret_cast<T *>(reinterpret_cast<char *>(sc) + 64 * kWaves);
+    *total = *reinterpret_cast<T *>(reinterpret_cast<char *>(sc) + kSlot * kWaves);
     __syncthreads();
     return ex;
   }
 };
 
-// LDS bytes the policy needs
+using DevBlock = DevBlockT<64>;
+using DevBlockS = DevBlockT<8>;  // the single-pass kernels: scan elements <= 8 bytes
+
+// LDS words the policies need
 constexpr int kBlockScratchU64 = 8 * (kWaves + 1);
+constexpr int kSmallScratchU64 = kWaves + 1;
 
 }  // namespace dmlc_amd

@@ -17,8 +17,8 @@ __global__ void __launch_bounds__(kThreads) csv_tile(CsvArgs a) {
   csv::tile<MODE>(a, sh, bk, blockIdx.x);
 }
 
-// 6 workgroups per CU: LDS in 512-byte granules, <= 53 of them (svm_fast_tile)
-static_assert(sizeof(fcsv::Shared) + kBlockScratchU64 * 8 <= 53 * 512, "csv_fast_tile LDS above the 6-workgroup budget");
+static_assert(sizeof(fcsv::Shared) + kSmallScratchU64 * 8 <= fast::kLdsBudget,
+              "csv_fast_tile LDS above the 6-workgroup budget (fast_common.h kLdsBudget)");
 
 #ifndef FCSV_MINW
 #define FCSV_MINW 6
@@ -26,24 +26,24 @@ static_assert(sizeof(fcsv::Shared) + kBlockScratchU64 * 8 <= 53 * 512, "csv_fast
 template <int MODE>
 __global__ void __launch_bounds__(kThreads, FCSV_MINW) csv_fast_tile(FastCsvArgs a) {
   __shared__ __attribute__((aligned(16))) fcsv::Shared sh;
-  __shared__ uint64_t scratch[kBlockScratchU64];
-  DevBlock bk{scratch};
+  __shared__ uint64_t scratch[kSmallScratchU64];
+  DevBlockS bk{scratch};
   fcsv::tile<MODE, false, 0>(a, sh, bk, blockIdx.x);
 }
 // integer DTypes (strtoll)
 template <int MODE>
 __global__ void __launch_bounds__(kThreads, FCSV_MINW) csv_fast_tile_int(FastCsvArgs a) {
   __shared__ __attribute__((aligned(16))) fcsv::Shared sh;
-  __shared__ uint64_t scratch[kBlockScratchU64];
-  DevBlock bk{scratch};
+  __shared__ uint64_t scratch[kSmallScratchU64];
+  DevBlockS bk{scratch};
   fcsv::tile<MODE, false, 1>(a, sh, bk, blockIdx.x);
 }
 // with a label and / or weight column
 template <int MODE>
 __global__ void __launch_bounds__(kThreads, FCSV_MINW) csv_fast_tile_sp(FastCsvArgs a) {
   __shared__ __attribute__((aligned(16))) fcsv::Shared sh;
-  __shared__ uint64_t scratch[kBlockScratchU64];
-  DevBlock bk{scratch};
+  __shared__ uint64_t scratch[kSmallScratchU64];
+  DevBlockS bk{scratch};
   fcsv::tile<MODE, true, 0>(a, sh, bk, blockIdx.x);
 }
 

@@ -10,6 +10,13 @@
 namespace dmlc_amd {
 namespace fast {
 
+// LDS of one single-pass workgroup.  gfx950 allocates LDS in 1280-byte
+// granules (160 KiB / 128): 6 workgroups per CU fit 21 granules each
+// (26,880 bytes), one byte more and the launch drops to 5 per CU (measured:
+// +32 bytes took svm_fast_tile from 1.84 to 2.04 ms).
+constexpr int kLdsGranule = 1280;
+constexpr int kLdsBudget = 21 * kLdsGranule;
+
 constexpr int kSegB = 64;                // bytes per thread (one 64-bit mask)
 constexpr int kTile = kThreads * kSegB;  // 16 KiB of text per tile
 constexpr int kPre = 64;                 // staged bytes before the tile (the segment before it)
@@ -471,18 +478,14 @@ DA_HD float wfloat32(const uint32_t w[4], const DecTables &tb, bool *ok) {
 // digits may not fit the form (caller falls back).
 // M: bit i set when window byte i is not '0'..'9' (bits 0-11 used)
 DA_HD bool wuint32m(const uint32_t w[4], uint32_t M, const DecTables &tb, uint64_t *out, bool *ok) {
+  (void)tb;
   const uint32_t b0 = w[0] & 0xFFu;
-  *ok = true;
-  if (b0 == '-') return false;
   const uint32_t s = b0 == '+' ? 1u : 0u;
   M = (M & 0xFFFu) | 0x1000u;
   const uint32_t L = (uint32_t)ctz32(M & ~s) - s;
-  if (L > 8u) {
-    *ok = false;
-    return true;
-  }
-  *out = digits_ra(w, s, L);
-  return true;
+  *ok = L <= 8u;  // branch-free, as wfloat32m
+  *out = digits_ra(w, s, L < 8u ? L : 8u);
+  return b0 != '-';
 }
 DA_HD bool wuint32(const uint32_t w[4], const DecTables &tb, uint64_t *out, bool *ok) {
   return wuint32m(w, nd4(w[0]) | (nd4(w[1]) << 4) | (nd4(w[2]) << 8), tb, out, ok);
@@ -524,8 +527,10 @@ struct TileCommon {
   alignas(16) uint8_t text[kStage];  // position p <-> text[p - tlo + kPre]
   uint64_t csl[kMaxCs + 1];           // chunk starts in [tlo, thi]
   uint64_t cfloor, cnext, base[4];    // last chunk start <= tlo, first beyond the list, output bases
+#ifdef FSVM_LB_DRAIN
   uint64_t lbw[4];                    // look-back: the inclusive prefix read by one lane
-  uint32_t ncs, c_first, tile, toomany, bad;
+#endif
+  uint32_t ncs, c_first, toomany, bad;
 };
 
 // Wave 0 (all 64 lanes): the chunk starts touching [tlo, thi].  The chunk of

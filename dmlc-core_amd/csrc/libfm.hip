@@ -21,14 +21,17 @@ __global__ void __launch_bounds__(kThreads) libfm_tile(LibfmArgs a) {
   fm::tile<MODE>(a, sh, bk, blockIdx.x);
 }
 
+static_assert(sizeof(fsvm::Shared) + kSmallScratchU64 * 8 <= fast::kLdsBudget,
+              "fm_fast_tile LDS above the 6-workgroup budget (fast_common.h kLdsBudget)");
+
 #ifndef FFM_MINW
 #define FFM_MINW 6
 #endif
 template <int MODE>
 __global__ void __launch_bounds__(kThreads, FFM_MINW) fm_fast_tile(FastSvmArgs a) {
   __shared__ __attribute__((aligned(16))) fsvm::Shared sh;
-  __shared__ uint64_t scratch[kBlockScratchU64];
-  DevBlock bk{scratch};
+  __shared__ uint64_t scratch[kSmallScratchU64];
+  DevBlockS bk{scratch};
   fsvm::tile<MODE, true>(a, sh, bk, blockIdx.x);
 }
 

@@ -22,10 +22,8 @@ __global__ void __launch_bounds__(kThreads) libsvm_tile(LibsvmArgs a) {
   svm::tile<MODE>(a, sh, bk, blockIdx.x);
 }
 
-// LDS is allocated in 512-byte granules: 6 workgroups per CU need <= 53 of
-// them (160 KiB / 6 = 27306 B), one byte more and the launch drops to 5
-static_assert(sizeof(fsvm::Shared) + kBlockScratchU64 * 8 <= 53 * 512,
-              "svm_fast_tile LDS above the 6-workgroup budget");
+static_assert(sizeof(fsvm::Shared) + kSmallScratchU64 * 8 <= fast::kLdsBudget,
+              "svm_fast_tile LDS above the 6-workgroup budget (fast_common.h kLdsBudget)");
 
 template <int MODE>
 #ifndef FSVM_MINW
@@ -33,12 +31,12 @@ template <int MODE>
 #endif
 __global__ void __launch_bounds__(kThreads, FSVM_MINW) svm_fast_tile(FastSvmArgs a) {
   __shared__ __attribute__((aligned(16))) fsvm::Shared sh;
-  __shared__ uint64_t scratch[kBlockScratchU64];
+  __shared__ uint64_t scratch[kSmallScratchU64];
 #ifdef FSVM_ABL_PAD_LDS  // occupancy experiment only: pad the workgroup's LDS
   __shared__ uint32_t pad[FSVM_ABL_PAD_LDS / 4];
   if (a.n == 1) pad[threadIdx.x] = 1, a.res[15] = pad[(threadIdx.x + 1) % kThreads];
 #endif
-  DevBlock bk{scratch};
+  DevBlockS bk{scratch};
   fsvm::tile<MODE>(a, sh, bk, blockIdx.x);
 }
 

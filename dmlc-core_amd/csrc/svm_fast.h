@@ -1011,7 +1011,7 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
     return ok ? v : slow_idx(o);
   };
 #ifndef FSVM_KB
-#define FSVM_KB 4
+#define FSVM_KB 3
 #endif
   constexpr int kB = FSVM_KB;  // runs per decoder decoded before the look-back
   static_assert(kB >= 1 && kB <= 5, "batch positions are packed 6 bits each");
