@@ -284,7 +284,9 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
       // begins at a blank field start (a field start always begins its run).
       // The run carried in from the segment before when that one ends in
       // blanks which follow a delimiter, a newline or a chunk start.
-      const uint64_t B = ~(D | N | L) & valid;
+      // A chunk start ends a blank run (the decoder would read past the
+      // chunk: bad) and, when blank, starts a run of its own (X).
+      const uint64_t B = ~(D | N | L) & valid, Bs = B & ~S, X = F & B & S;
       uint32_t cin = 0;
       if (P > 0 && !(S & 1u)) {
         const uint64_t nb1 = sh.u.m.d[tid] | n1 | l1;  // non-blank bytes of the segment before
@@ -293,18 +295,19 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
             bad = 1;  // 64 blanks in a row: beyond this carry, the exact kernels take it
           } else {
             const uint32_t j = 63u - (uint32_t)clz64(nb1);
-            const uint64_t x = P - 64u + j + 1u;  // the run's first byte
-            bool cs = x == sh.c.cfloor;
-            for (uint32_t i = 0; i < sh.c.ncs; ++i) cs = cs || sh.c.csl[i] == x;
+            const uint64_t x0 = P - 64u + j + 1u;  // the trailing run's first byte
+            bool cs = x0 <= sh.c.cfloor && sh.c.cfloor < P;  // a chunk (and row) starts inside the run
+            for (uint32_t i = 0; i < sh.c.ncs; ++i) cs = cs || (x0 <= sh.c.csl[i] && sh.c.csl[i] < P);
             cin = (((n1 | l1) >> j) & 1u) || cs ? 1u : 0u;
           }
         }
       }
-      uint32_t cout;
-      const uint64_t land = add_carry(B, F & B, cin, &cout) & ~B;  // first non-blank after a blank field start
+      uint32_t c1, c2;
+      const uint64_t land = (add_carry(Bs, F & Bs, cin, &c1) | add_carry(Bs, X << 1, 0u, &c2)) & ~Bs;
       // the run reaches a newline, a chunk start or the text end: ParseFloat /
       // strtoll would skip on into the next line (csv_parser.h:99-105)
       if (land & (N | S | ~valid)) bad = 1;
+      const uint32_t cout = c1 | c2 | (uint32_t)(X >> 63);
       if (cout && (P + 64 >= a.n || t.is_cs(P + 64))) bad = 1;
       if constexpr (VT == 0) {
         // a blank field ending at a delimiter is ParseFloat's 0 (it consumed the blanks)
@@ -314,7 +317,9 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
         // the field is then a missing value (csv_parser.h:115-118)
         const uint64_t C = (F & D) | (land & D);
         const uint64_t G = (uint64_t)sh.gw[2 * tid] | ((uint64_t)sh.gw[2 * tid + 1] << 32);
-        const uint64_t Gn = (G >> 1) | ((uint64_t)(sh.gw[2 * tid + 2] & 1u) << 63);  // next byte a digit
+        // next byte a digit of the same chunk (strtoll stops at the chunk end)
+        const uint64_t Gn = ((G >> 1) | ((uint64_t)(sh.gw[2 * tid + 2] & 1u) << 63)) & ~(S >> 1) &
+                            ~((uint64_t)t.is_cs(P + 64) << 63);
         T = C & G;
         for (uint64_t m = C & ~G & Gn; m; m &= m - 1) {
           const uint32_t b = sh.c.text[kPre + tid * kSegB + ctz64(m)];

@@ -498,12 +498,12 @@ def test_emu_csv_fast_blanks_and_ints(vt):
     rng = np.random.default_rng({"f32": 31, "i32": 32, "i64": 33}[vt])
     paths = {"fast": 0, "exact": 0}
     vmap = {"f32": 0, "i32": 1, "i64": 2}
-    for it in range(24):
+    for it in range(36):
         big = it % 6 == 5
         violate = (not big) and rng.random() < 0.3
         data = fuzz_text.blank_csv(rng, 1500 if big else int(rng.integers(1, 40)), 40 if big else 20,
                                    ints=vt != "f32" or rng.random() < 0.2, violate=violate)
-        offs = fuzz_text.random_cuts(rng, data, 5)
+        offs = fuzz_text.random_cuts(rng, data, 5, anywhere=it % 3 == 1)  # cuts inside blank runs too
         kw = {"value_type": vmap[vt]}
         if vt != "f32" and rng.random() < 0.3:
             kw["weight_column"] = int(rng.integers(0, 3))  # an ordinary column for integer DTypes
@@ -516,3 +516,23 @@ def test_emu_csv_fast_blanks_and_ints(vt):
             assert diff(h, o) == [], (it, diff(h, o), data[:300])
         paths[h["path"]] += 1
     assert paths["fast"] >= 12, paths
+
+
+@pytest.mark.parametrize("vt", [0, 1, 2])
+def test_emu_csv_chunk_cut_edges(vt):
+    """Chunk cuts inside blank runs and between a sign and its digits: the
+    decoders stop at the chunk end (the reference's chunk buffer), so a blank
+    field reaching it, or a sign whose digit lies in the next chunk, must not
+    borrow the next chunk's bytes."""
+    cases = [(b"1,-5,2\n", [0, 3, 7]), (b"1,+7\n4\n", [0, 3, 8]), (b"1,  \n 2,3\n", [0, 3, 11]),
+             (b"1, 2,3\n", [0, 3, 7]), (b"5, ,  6\n", [0, 4, 8]), (b"-\n9,1\n", [0, 1, 6]),
+             (b"1|  |2\n", [0, 3, 7]), (b" 7, 8\n 9\n", [0, 1, 10])]
+    for data, offs in cases:
+        kw = {"value_type": vt}
+        okw = {"value_kind": vt}
+        o = po.parse_chunks(data, offs, fmt=po.CSV, delimiter="|" if b"|" in data else ",", **okw)
+        h = pyemu.parse(data, offs, "csv", delimiter="|" if b"|" in data else ",", **kw)
+        failed = check_fail(h, "csv", offs)
+        assert (o["status"] != 0) == failed, (data, offs, o["msg"], h["error"])
+        if not failed:
+            assert diff(h, o) == [], (data, offs, diff(h, o))

@@ -422,36 +422,6 @@ def test_gpu_fast_synthetic_vs_oracle(dm):
     assert diff(h, o) == []
 
 
-def test_gpu_fast_equals_exact_bench_size(dm):
-    """Bench-size input (BASELINE config 2, 1M rows x 128 nnz): the single-pass
-    kernel and the exact kernels agree bit for bit (the exact kernels are
-    pinned to the oracle above); plus size-independent CSR properties."""
-    import torch
-    text, _ = synth.rows(synth.LIBSVM, 1 << 20, 128, seed=1)
-    starts = dm.text_chunk_starts(text)
-    d_text = torch.from_numpy(text).cuda()
-    d_cs = torch.from_numpy(starts).cuda()
-    outs = {}
-    for exact in (False, True):
-        p = dm.DeviceParser("libsvm", flags=dm.FLAG_EXACT if exact else 0)
-        out = p.parse(d_text, d_cs)
-        assert out["error"] == 0 and out["path"] == (1 if exact else 0)
-        outs[exact] = out
-    c = outs[False]["counts"]
-    assert c[:7] == outs[True]["counts"][:7]
-    assert c[dm.ROWS] == 1 << 20 and c[dm.INDEX] == 128 << 20 and c[dm.VALUE] == 128 << 20
-    for k in ("offset", "label", "index", "value"):
-        a, b = outs[False][k], outs[True][k]
-        assert torch.equal(a.view(torch.int32) if a.dtype == torch.float32 else a,
-                           b.view(torch.int32) if b.dtype == torch.float32 else b), k
-    off = outs[False]["offset"]
-    assert bool((off[1:] - off[:-1] == 128).all())
-    idx = outs[False]["index"].view(-1, 128).to(torch.int64)
-    assert bool((idx[:, 1:] > idx[:, :-1]).all())  # generator: strictly increasing ids
-    v = outs[False]["value"]
-    assert bool(((v >= 0) & (v < 1)).all())
-
-
 # ------------------------------------------------- single-pass CSV path --
 
 
@@ -483,35 +453,6 @@ def test_gpu_csv_fast_multi_tile_vs_oracle(dm):
         offs = fuzz_text.random_cuts(rng, data, int(rng.integers(0, 30)), anywhere=it % 3 == 1)
         h = _gpu_vs_oracle_paths(dm, data, offs, fmt=po.CSV)
         assert h["path"] == "fast", it
-
-
-def test_gpu_csv_fast_equals_exact_bench_size(dm):
-    """BASELINE config 3 (1M rows x 256 float columns): the single-pass CSV
-    kernel and the exact kernels agree bit for bit; CSR properties."""
-    import torch
-    text, _ = synth.rows(synth.CSV, 1 << 20, 256, seed=1)
-    starts = dm.text_chunk_starts(text)
-    d_text = torch.from_numpy(text).cuda()
-    d_cs = torch.from_numpy(starts).cuda()
-    outs = {}
-    for exact in (False, True):
-        p = dm.DeviceParser("csv", flags=dm.FLAG_EXACT if exact else 0)
-        out = p.parse(d_text, d_cs)
-        assert out["error"] == 0 and out["path"] == (1 if exact else 0)
-        outs[exact] = out
-    c = outs[False]["counts"]
-    assert c[:7] == outs[True]["counts"][:7]
-    assert c[dm.ROWS] == 1 << 20 and c[dm.INDEX] == 256 << 20 and c[dm.VALUE] == 256 << 20
-    for k in ("offset", "index", "value"):
-        a, b = outs[False][k], outs[True][k]
-        assert torch.equal(a.view(torch.int32) if a.dtype == torch.float32 else a,
-                           b.view(torch.int32) if b.dtype == torch.float32 else b), k
-    off = outs[False]["offset"]
-    assert bool((off[1:] - off[:-1] == 256).all())
-    idx = outs[False]["index"].view(-1, 256).to(torch.int64)
-    assert bool((idx == torch.arange(256, device=idx.device)).all())
-    v = outs[False]["value"]
-    assert bool(((v >= -1) & (v < 1)).all())
 
 
 def test_gpu_sharded_parts_concat(dm):
@@ -546,41 +487,6 @@ def test_gpu_config4_wide_rows_vs_oracle(dm):
         assert o["status"] == 0 and h["error"] == 0 and h["path"] == "fast", kw
         assert diff(h, o) == [], kw
         assert h["counts"][dm.INDEX] == 6000 * 2048
-
-
-def test_gpu_config4_full_size_fast_equals_exact(dm):
-    """Config 4 at full size (1M rows x 2048 nnz, ~37 GB of text): a 64k-row
-    block repeated 16 times on the device (the repeats shift the tile / row
-    alignment), single-pass kernel == exact kernels bit for bit, plus CSR
-    properties (2048 per row, strictly increasing ids, values in [0, 1))."""
-    import torch
-    blk, _ = synth.rows(synth.LIBSVM, 1 << 16, 2048, seed=1)
-    d_blk = torch.from_numpy(blk).cuda()
-    d_text = d_blk.repeat(16)
-    del d_blk
-    starts = dm.text_chunk_starts(blk)
-    reps = [torch.from_numpy(starts[:-1].astype(np.int64)) + r * blk.size for r in range(16)]
-    d_cs = torch.cat(reps + [torch.tensor([16 * blk.size])]).cuda()
-    outs = {}
-    for exact in (False, True):
-        p = dm.DeviceParser("libsvm", flags=dm.FLAG_EXACT if exact else 0)
-        out = p.parse(d_text, d_cs)
-        assert out["error"] == 0 and out["path"] == (1 if exact else 0)
-        outs[exact] = out
-    c = outs[False]["counts"]
-    assert c[:7] == outs[True]["counts"][:7]
-    assert c[dm.ROWS] == 1 << 20 and c[dm.INDEX] == 2048 << 20 and c[dm.VALUE] == 2048 << 20
-    for k in ("offset", "label", "index", "value"):
-        a, b = outs[False][k], outs[True][k]
-        assert torch.equal(a.view(torch.int32) if a.dtype == torch.float32 else a,
-                           b.view(torch.int32) if b.dtype == torch.float32 else b), k
-    del outs[True]
-    off = outs[False]["offset"]
-    assert bool((off[1:] - off[:-1] == 2048).all())
-    idx = outs[False]["index"].view(-1, 2048)
-    assert bool((idx[:, 1:].to(torch.int64) > idx[:, :-1].to(torch.int64)).all())
-    v = outs[False]["value"]
-    assert bool(((v >= 0) & (v < 1)).all())
 
 
 def test_gpu_max_index_flag(dm):
@@ -667,8 +573,8 @@ def test_gpu_libfm_synthetic_vs_oracle(dm):
     assert len(data) > 1 << 20
     for kw in ({}, {"indexing_mode": 1}, {"indexing_mode": -1}, {"index_bits": 64, "tile_bytes": 4096}):
         h = _oracle_vs_gpu(dm, data, _random_chunks(rng, data, 12), po.LIBFM, **kw)
-        # the single-pass kernel unless indexing_mode < 0 (per-chunk detection)
-        assert h["path"] == ("exact" if kw.get("indexing_mode", 0) < 0 else "fast"), kw
+        # the single-pass kernel in every mode (indexing_mode < 0: per-unit fix-up, svm_fast.h umin_fix)
+        assert h["path"] == "fast", kw
         assert len(h["field"]) == len(h["index"]) > 100000
         he = _oracle_vs_gpu(dm, data, [0, len(data)], po.LIBFM, exact=True, **kw)
         assert he["path"] == "exact"
@@ -922,3 +828,49 @@ def test_gpu_fast_indexing_mode_auto_vs_oracle(dm, nthread):
         offs = fuzz_text.random_cuts(rng, data, 5)
         h = _gpu_vs_oracle_paths(dm, data, offs, fmt=po.LIBFM, indexing_mode=-1, nthread=nthread)
         assert h["path"] == "fast", it
+
+
+FULL = load_json("synth_full.json") if __import__("os").path.exists(
+    __import__("os").path.join(__import__("os").path.dirname(__file__), "golden", "synth_full.json")) else {}
+
+
+@pytest.mark.parametrize("name", sorted(FULL))
+def test_gpu_fullsize_vs_reference_hashes(dm, name):
+    """BASELINE configs 2-5 at full size (config 5: each of bench.py's 8
+    per-rank shards), generated and chunked exactly as the bench does, parsed
+    on the GPU's default path, every output array hashed and compared with the
+    SHA-256 the GENUINE reference's ParseBlock produced for the same chunks
+    (tests/golden/make_fullsize.py, oracle/_ref).  The text streams to the
+    device chunk by chunk and the arrays stream back in slices, so host memory
+    stays bounded (config 4 is 37 GB of text)."""
+    import hashlib
+    import sys
+    import torch
+    sys.path.insert(0, __import__("os").path.join(__import__("os").path.dirname(__file__), "golden"))
+    import make_fullsize as mf
+    fx = FULL[name]
+    sfmt, _, rows, width, row0 = mf.CONFIGS[name]
+    d_text = torch.empty(fx["input_bytes"], dtype=torch.uint8, device="cuda")
+    starts, pos = [0], 0
+    for i, ch in enumerate(mf.stream_chunks(sfmt, rows, width, row0, max(1, (16 << 20) // (width * 16)))):
+        if i == 0:
+            assert hashlib.sha256(ch).hexdigest() == fx["first_chunk_sha256"]
+        d_text[pos:pos + len(ch)].copy_(torch.frombuffer(bytearray(ch), dtype=torch.uint8))
+        pos += len(ch)
+        starts.append(pos)
+    assert pos == fx["input_bytes"] and len(starts) - 1 == fx["chunks"]
+    d_cs = torch.tensor(starts, dtype=torch.int64, device="cuda")
+    p = dm.DeviceParser(fx["format"])
+    out = p.parse(d_text, d_cs)
+    del d_text
+    assert out["error"] == 0 and out["path"] == 0, (out["error"], out["path"])
+    c = out["counts"]
+    for k, slot in (("offset", dm.ROWS), ("label", dm.LABEL), ("weight", dm.WEIGHT), ("qid", dm.QID),
+                    ("field", dm.FIELD), ("index", dm.INDEX), ("value", dm.VALUE)):
+        n = c[slot] + (1 if k == "offset" else 0)
+        assert n == fx["sizes"][k], (k, n, fx["sizes"][k])
+        h = hashlib.sha256()
+        t = out[k]
+        for a in range(0, n, 1 << 26):
+            h.update(t[a:min(n, a + (1 << 26))].cpu().numpy().tobytes())
+        assert h.hexdigest() == fx["sha256"][k], k
