@@ -75,7 +75,12 @@ struct FastSvmArgs {
   uint32_t *gate;       // != 0: input left the grammar -> exact path
   unsigned long long *err;  // first error of this path
   uint64_t *res;        // dmlc_amd_result counts (written by the last tile)
+  uint32_t *ticket;     // persistent launch: tiles handed out past the first gridDim.x (zeroed per launch)
 };
+
+// look-back words per single-pass tile (fast_common.h: status + 4 prefix words);
+// the persistent launch's ticket word follows them
+constexpr uint64_t kFastLbWords = 5;
 
 // Single-pass uniform-grammar CSV kernel (csv_fast.h).
 constexpr int kLabShards = 64;  // FastCsvArgs::labsum shards, one 64-byte line each

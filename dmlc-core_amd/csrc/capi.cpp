@@ -242,6 +242,7 @@ int dmlc_amd_parse(const void *d_text, uint64_t nbytes, const uint64_t *d_chunk_
     // the chunk table, or the workspace's when the caller passes none
     f.chunk_tab = d_chunk_table ? d_chunk_table : (prm->indexing_mode < 0 ? chunk_sink : nullptr);
     f.lb = lb;
+    f.ticket = reinterpret_cast<uint32_t *>(lb + nft * dmlc_amd::kFastLbWords);  // zeroed with lb
     f.qsum = labsum;
     f.umin = fast_min;
     f.gate = ctl;

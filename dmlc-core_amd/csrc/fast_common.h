@@ -876,7 +876,7 @@ DA_HDF uint32_t look_back(uint64_t *lb, uint32_t ntiles, uint32_t k, const uint3
 }
 #endif
 // words of look-back state per tile the launch must zero (status + prefix)
-constexpr uint64_t kLbWords = 5;
+constexpr uint64_t kLbWords = kFastLbWords;  // args.h: the launcher sizes the workspace by it
 
 }  // namespace fast
 }  // namespace dmlc_amd

@@ -61,6 +61,25 @@ DA_HD void atomic_min_u64(unsigned long long *p, unsigned long long v) {
 #endif
 }
 
+// a text byte from global memory, typed as such: a read that may come from
+// LDS or global memory (the fast kernels' at()) would otherwise become one
+// flat load of a selected pointer, which waits on both counters
+DA_HD uint32_t gbyte(const uint8_t *t, uint64_t p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return *((const __attribute__((address_space(1))) uint8_t *)t + p);
+#else
+  return t[p];
+#endif
+}
+
+DA_HD uint32_t gridDim_x() {  // workgroups of the launch (0 on the host)
+#if defined(__HIP_DEVICE_COMPILE__)
+  return gridDim.x;
+#else
+  return 0;
+#endif
+}
+
 DA_HD uint32_t atomic_add_u32(uint32_t *p, uint32_t v) {  // returns the old value
 #if defined(__HIP_DEVICE_COMPILE__)
   return atomicAdd(p, v);

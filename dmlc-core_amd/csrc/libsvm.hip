@@ -29,6 +29,9 @@ template <int MODE>
 #ifndef FSVM_MINW
 #define FSVM_MINW 6  // workgroups per CU the fill kernel is register-budgeted for
 #endif
+#ifndef FSVM_PERSIST
+#define FSVM_PERSIST 0  // workgroups loop over tiles (svm_fast.h tile_p)
+#endif
 __global__ void __launch_bounds__(kThreads, FSVM_MINW) svm_fast_tile(FastSvmArgs a) {
   __shared__ __attribute__((aligned(16))) fsvm::Shared sh;
   __shared__ uint64_t scratch[kSmallScratchU64];
@@ -37,7 +40,40 @@ __global__ void __launch_bounds__(kThreads, FSVM_MINW) svm_fast_tile(FastSvmArgs
   if (a.n == 1) pad[threadIdx.x] = 1, a.res[15] = pad[(threadIdx.x + 1) % kThreads];
 #endif
   DevBlockS bk{scratch};
+#if FSVM_PERSIST
+  // persistent: the first tile is the workgroup's index (dispatch order makes
+  // every lower one resident first), later ones come from the ticket
+  if (a.skip_if_gated && *a.gate) return;  // fill phase after an exact-path count: block-uniform
+  fsvm::init_tables(sh, bk);
+  fast::StageRegs sr;
+  uint32_t k = blockIdx.x;
+  fast::stage_issue(a.text, a.n, (uint64_t)k * fast::kTile, sr, bk);
+  while (k < a.ntiles) {
+    k = fsvm::tile_p<MODE, false, true>(a, sh, bk, k, sr);
+    bk.sync();  // every thread is done with the tile's LDS
+  }
+#else
   fsvm::tile<MODE>(a, sh, bk, blockIdx.x);
+#endif
+}
+
+// workgroups of a persistent single-pass launch: what the device holds at
+// once (the occupancy calculator, capped at the 6 per CU the LDS budget
+// allows), never more than the tiles
+template <class K>
+uint32_t persistent_grid(K kernel, uint32_t ntiles) {
+  static int cache_dev[64], cache_n[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return ntiles;
+  if (cache_n[dev] == 0 || cache_dev[dev] != dev + 1) {
+    int cus = 0, per = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, kThreads, 0) != hipSuccess || cus < 1 || per < 1)
+      return ntiles;
+    cache_n[dev] = cus * (per < 6 ? per : 6);
+    cache_dev[dev] = dev + 1;
+  }
+  return (uint32_t)cache_n[dev] < ntiles ? (uint32_t)cache_n[dev] : ntiles;
 }
 
 // fill phase after a count phase that fell back to the exact kernels: the
@@ -95,18 +131,19 @@ hipError_t launch_libsvm(const LibsvmArgs &a, const FastSvmArgs &f, bool use_fas
     return e;  // rows no tile writes are filled by chunk_fixup_kernel
   if (use_fast) {
     if ((e = hipMemsetAsync(f.err, 0xFF, sizeof(uint64_t), s)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(f.lb, 0, (size_t)f.ntiles * fast::kLbWords * sizeof(uint64_t), s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(f.lb, 0, ((size_t)f.ntiles * fast::kLbWords + 1) * sizeof(uint64_t), s)) != hipSuccess)
+      return e;  // + the ticket word
     if ((e = hipMemsetAsync(f.qsum, 0, kLabShards * 8 * sizeof(uint64_t), s)) != hipSuccess) return e;
     if (phase == kPhaseCount) {
       prof_mark(0, s, "svm_fast_tile<1>");
-      svm_fast_tile<1><<<f.ntiles, kThreads, 0, s>>>(f);
+      svm_fast_tile<1><<<FSVM_PERSIST ? persistent_grid(svm_fast_tile<1>, f.ntiles) : f.ntiles, kThreads, 0, s>>>(f);
       prof_mark(1, s, "svm_fast_tile<1>");
     } else {
       if (f.indexing_mode < 0 &&
           (e = hipMemsetAsync(f.umin, 0xFF, (size_t)f.nchunk * sizeof(uint64_t), s)) != hipSuccess)
         return e;
       prof_mark(0, s, "svm_fast_tile<2>");
-      svm_fast_tile<2><<<f.ntiles, kThreads, 0, s>>>(f);
+      svm_fast_tile<2><<<FSVM_PERSIST ? persistent_grid(svm_fast_tile<2>, f.ntiles) : f.ntiles, kThreads, 0, s>>>(f);
       prof_mark(1, s, "svm_fast_tile<2>");
     }
     qid_fix_kernel<<<1, 256, 0, s>>>(f.qsum, res, gate, phase != kPhaseCount ? f.chunk_tab : nullptr, f.nchunk);

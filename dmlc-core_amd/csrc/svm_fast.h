@@ -143,6 +143,7 @@ struct Shared {  // LDS of one workgroup
   uint32_t gw[2 * kThreads + 2];  // digit plane as words: 2t, 2t+1 segment t; 2 kThreads: the post-halo
   uint64_t pend[kTile / kPassRuns + 2];  // packed inclusive counts at the end of each pass
   uint32_t npass;
+  uint32_t next;   // persistent form: the next tile id
   uint32_t nq;     // qid runs of the tile
   uint32_t hashy;  // a byte outside the grammar: comments to blank (pass 1)
 };
@@ -397,6 +398,31 @@ struct CommentFnCompose {  // a then b
 DA_HD void blank_bytes(uint8_t *p, uint64_t m) {
   for (; m; m &= m - 1) p[ctz64(m)] = ' ';
 }
+// The comment masks of a segment in the grammar, from its classification
+// planes (no '#'; the other bytes are blanks).
+DA_HD CmtMasks plane_cmt_masks(uint64_t D, uint64_t N, uint64_t C) {
+  return CmtMasks{0, N & ~C, ~(D | N | C), D};
+}
+// The comment masks of the 64 staged bytes at p by the whole wave: lane =
+// byte, one ballot per mask (all lanes; p wave-uniform).
+template <class BK>
+DA_HDF CmtMasks wave_cmt_masks(const uint8_t *p, BK &bk) {
+  const uint32_t b = p[bk.tid() & (kWave - 1)];
+  CmtMasks k;
+  k.h = bk.ballot(b == '#');
+  k.nl = bk.ballot(is_nl(b));
+  k.bl = bk.ballot(is_blank(b));
+  k.dg = bk.ballot(is_digitchar(b));
+  return k;
+}
+// Lane `owner`'s mask M blanks bytes of the 64 staged bytes at p (p wave
+// uniform), by the whole wave.
+template <class BK>
+DA_HDF void wave_blank(uint8_t *p, uint64_t M, uint32_t owner, BK &bk) {
+  const uint64_t Ms = bk.shfl(M, (int)owner);
+  const uint32_t lane = (uint32_t)bk.tid() & (kWave - 1);
+  if ((Ms >> lane) & 1u) p[lane] = ' ';
+}
 // the comment bytes of a segment (A '#', B comment ends, cin open before it);
 // *co: open after it
 DA_HD uint64_t comment_mask(uint64_t A, uint64_t B, uint32_t cin, uint32_t *co) {
@@ -416,18 +442,35 @@ DA_HD uint64_t cs_bits(const TileCommon &c, uint64_t lo) {
 // Blanks the comments of the staged text (pre-halo, tile, post-halo); all
 // threads.  Returns 1 (gate) when the tile after this one cannot see from its
 // pre-halo that a comment is open at its start.
+//
+// A segment in the grammar (raw = 0) has no '#': its masks come from its
+// classification planes D, N, C; the segments holding other bytes are read
+// byte by byte, one segment at a time by their wave (lane = byte), and the
+// comment bytes are blanked the same way -- per-lane byte loops would run
+// every wave through the slowest lane's segment.
 template <class BK>
-DA_HDF uint32_t comment_erase(uint64_t tlo, uint64_t thi, uint64_t n, TileCommon &c, uint32_t *note, BK &bk) {
+DA_HDF uint32_t comment_erase(uint64_t tlo, uint64_t thi, uint64_t n, TileCommon &c, uint32_t *note, BK &bk,
+                              uint64_t D, uint64_t N, uint64_t C, bool raw) {
   const int tid = bk.tid();
+  const uint32_t lane = (uint32_t)tid & (kWave - 1), wbase = (uint32_t)tid - lane;
   uint8_t *txt = c.text;
   const uint64_t P = tlo + (uint64_t)tid * kSegB;
-  const CmtMasks k = comment_masks(txt + kPre + tid * kSegB);
+  CmtMasks k = plane_cmt_masks(D, N, C);
+  for (uint64_t m = bk.ballot(raw); m; m &= m - 1) {  // wave-uniform
+    const uint32_t s = (uint32_t)ctz64(m);
+    const CmtMasks kk = wave_cmt_masks(txt + kPre + (wbase + s) * kSegB, bk);
+    if (lane == s) k = kk;
+  }
+  // wave 0: the pre-halo's masks; wave 3: the post-halo's
+  CmtMasks kh{0, 0, 0, 0}, kp[kPost / kSegB];
+  if (tid < kWave && tlo > 0) kh = wave_cmt_masks(txt, bk);
+  if (tid >= kThreads - kWave)
+    for (int s = 0; s < kPost / kSegB; ++s) kp[s] = wave_cmt_masks(txt + kPre + kTile + s * kSegB, bk);
   const uint64_t S = cs_bits(c, P);
   // the pre-halo read on its own (reach-in 0, no comment open before it): the
   // tile start's reach and comment state, as the tile before checks them
   uint64_t hA = 0, hB = 0;
   if (tid == 0 && tlo > 0) {
-    const CmtMasks kh = comment_masks(txt);
     const uint64_t Sh = cs_bits(c, tlo - kPre);
     uint32_t r0;
     (void)reach_of(kh, Sh, 0u, &r0);
@@ -451,28 +494,33 @@ DA_HDF uint32_t comment_erase(uint64_t tlo, uint64_t thi, uint64_t n, TileCommon
   const uint32_t cin = (pre >> ((*note >> 2) & 1u)) & 1u;
   uint32_t co, gate = 0;
   const uint64_t M = comment_mask(A, B, cin, &co);
-  blank_bytes(txt + kPre + tid * kSegB, M);
+  for (uint64_t m = bk.ballot(M != 0); m; m &= m - 1) {  // wave-uniform
+    const uint32_t s = (uint32_t)ctz64(m);
+    wave_blank(txt + kPre + (wbase + s) * kSegB, M, s, bk);
+  }
   uint32_t changed = M != 0;  // bit 0: my segment, bit 1: the pre-halo, bit 2: the post-halo
-  if (tid == 0 && tlo > 0) {
+  if (tid < kWave && tlo > 0) {  // wave 0: lane 0's pre-halo comment bytes
     uint32_t ch;
     const uint64_t Mh = comment_mask(hA, hB, 0u, &ch);
-    blank_bytes(txt, Mh);
-    if (Mh) changed |= 2u;
+    wave_blank(txt, Mh, 0u, bk);
+    if (tid == 0 && Mh) changed |= 2u;
   }
-  if (tid == kThreads - 1) {
-    if (thi < n && P + kSegB == thi && !(cs_bits(c, thi) & 1u) && co != f_next) gate = 1;
-    uint32_t ci = co, ri;
-    (void)reach_of(k, S, r, &ri);
-    for (int s = 0; s < kPost / kSegB; ++s) {
-      const CmtMasks kp = comment_masks(txt + kPre + kTile + s * kSegB);
-      const uint64_t Sp = cs_bits(c, tlo + kTile + (uint64_t)s * kSegB);
-      uint64_t Ap, Bp;
-      comment_ab(kp, Sp, ri, &Ap, &Bp);
-      (void)reach_of(kp, Sp, ri, &ri);
-      const uint64_t Mp = comment_mask(Ap, Bp, ci, &ci);
-      blank_bytes(txt + kPre + kTile + s * kSegB, Mp);
-      if (Mp) changed |= 4u;
+  if (tid >= kThreads - kWave) {  // wave 3: lane 63's post-halo comment bytes
+    uint64_t Mp[kPost / kSegB] = {0, 0};
+    if (tid == kThreads - 1) {
+      if (thi < n && P + kSegB == thi && !(cs_bits(c, thi) & 1u) && co != f_next) gate = 1;
+      uint32_t ci = co, ri;
+      (void)reach_of(k, S, r, &ri);
+      for (int s = 0; s < kPost / kSegB; ++s) {
+        const uint64_t Sp = cs_bits(c, tlo + kTile + (uint64_t)s * kSegB);
+        uint64_t Ap, Bp;
+        comment_ab(kp[s], Sp, ri, &Ap, &Bp);
+        (void)reach_of(kp[s], Sp, ri, &ri);
+        Mp[s] = comment_mask(Ap, Bp, ci, &ci);
+        if (Mp[s]) changed |= 4u;
+      }
     }
+    for (int s = 0; s < kPost / kSegB; ++s) wave_blank(txt + kPre + kTile + s * kSegB, Mp[s], kWave - 1, bk);
   }
   return gate | (changed << 1);
 }
@@ -779,23 +827,29 @@ FSVM_COLD bool slow_uint(const uint8_t *text, uint64_t q, uint64_t lim, int wide
 // 0..15, OR-ed into slot 0) and of the 16 bytes after the tile (bit 2: lane
 // kWave): the LDS planes and digit-plane words; returns the segment's grammar
 // flag.  `first`: pass 0, which also notes bytes outside the grammar.
+// Segment seg's masks m (classify64_lut's form) into the planes and the
+// digit-plane words, "qid:" tokens cleaned; returns its grammar flag.
+template <bool FM, class At>
+DA_HDF uint32_t commit_seg(const Tile &t, Shared &sh, int seg, At at, bool first, Masks m) {
+  uint32_t bad = 0;
+  const uint64_t P0 = t.tlo + (uint64_t)seg * kSegB;
+  if ((m.n & m.c) || ((m.c & 1) && P0 > 0 && is_qid_letter(at(P0 - 1)))) {  // letters: "qid:" tokens
+    if (FM || !qid_clean(P0, &m.n, &m.c, P0 > 0 && is_qid_letter(at(P0 - 1)), at)) bad = 1;
+  }
+  sh.gw[2 * seg] = (uint32_t)m.g;
+  sh.gw[2 * seg + 1] = (uint32_t)(m.g >> 32);
+  sh.u.m.d[seg + 1] = m.d;
+  sh.u.m.n[seg + 1] = m.n;
+  sh.u.m.c[seg + 1] = m.c;
+  bad |= m.bad;
+  if (!FM && first && m.bad) sh.hashy = 1;
+  return bad;
+}
+
 template <bool FM, class At>
 DA_HDF uint32_t classify_tile(const Tile &t, Shared &sh, int tid, At at, bool first, uint32_t parts) {
   uint32_t bad = 0;
-  if (parts & 1u) {
-    Masks m = classify64_lut(sh.c.text + kPre + tid * kSegB, sh.cls);
-    const uint64_t P0 = t.tlo + (uint64_t)tid * kSegB;
-    if ((m.n & m.c) || ((m.c & 1) && P0 > 0 && is_qid_letter(at(P0 - 1)))) {  // letters: "qid:" tokens
-      if (FM || !qid_clean(P0, &m.n, &m.c, P0 > 0 && is_qid_letter(at(P0 - 1)), at)) bad = 1;
-    }
-    sh.gw[2 * tid] = (uint32_t)m.g;
-    sh.gw[2 * tid + 1] = (uint32_t)(m.g >> 32);
-    sh.u.m.d[tid + 1] = m.d;
-    sh.u.m.n[tid + 1] = m.n;
-    sh.u.m.c[tid + 1] = m.c;
-    bad |= m.bad;
-    if (!FM && first && m.bad) sh.hashy = 1;
-  }
+  if (parts & 1u) bad = commit_seg<FM>(t, sh, tid, at, first, classify64_lut(sh.c.text + kPre + tid * kSegB, sh.cls));
   if ((parts & 4u) && tid == kWave) {  // digits of the 16 bytes after the tile (windows of my last runs)
     uint32_t g = 0;
 #pragma unroll
@@ -831,25 +885,57 @@ DA_HDF uint32_t classify_tile(const Tile &t, Shared &sh, int tid, At at, bool fi
 template <class BK>
 DA_HDF uint32_t comments_reclassify(const Tile t, Shared &sh, uint32_t bad0, BK &bk) {
   const int tid = bk.tid();
+  const uint32_t lane = (uint32_t)tid & (kWave - 1), wbase = (uint32_t)tid - lane;
   const FastSvmArgs &a = *t.a;
-  const uint32_t e = comment_erase(t.tlo, t.thi, a.n, sh.c, &sh.hashy, bk);
+  const uint32_t e = comment_erase(t.tlo, t.thi, a.n, sh.c, &sh.hashy, bk, sh.u.m.d[tid + 1], sh.u.m.n[tid + 1],
+                                   sh.u.m.c[tid + 1], bad0 != 0);
   if (e & 12u) atomic_or_u32(&sh.hashy, (e & 12u) << 1);  // pre-halo / post-halo blanked: note bits 3 / 4
   if (tid == 0 && (e & 4u)) sh.u.m.d[0] = sh.u.m.n[0] = sh.u.m.c[0] = 0;
   bk.sync();
   auto at = [&](uint64_t p) -> uint32_t {
     if (p >= a.n) return 0u;
-    return p + kPre >= t.tlo ? (uint32_t)sh.c.text[p - t.tlo + kPre] : (uint32_t)a.text[p];
+    return p + kPre >= t.tlo ? (uint32_t)sh.c.text[p - t.tlo + kPre] : gbyte(a.text, p);
   };
+  // the blanked segments classified again, each by its wave (lane = byte)
+  uint32_t bad = bad0;
+  for (uint64_t m = bk.ballot((e >> 1) & 1u); m; m &= m - 1) {  // wave-uniform
+    const uint32_t sg = wbase + (uint32_t)ctz64(m);
+    const uint32_t x = sh.cls[sh.c.text[kPre + sg * kSegB + lane]];
+    Masks mm;
+    mm.d = bk.ballot(x & 1u);
+    mm.g = bk.ballot((x >> 8) & 1u);
+    mm.n = bk.ballot((x >> 16) & 1u);
+    mm.c = bk.ballot((x >> 24) & 1u);
+    mm.bad = (mm.g & ~mm.d) != 0;
+    if (sg == (uint32_t)tid) bad = commit_seg<false>(t, sh, tid, at, false, mm);
+  }
   const uint32_t note = sh.hashy;
-  const uint32_t parts = ((e >> 1) & 1u) | ((note >> 2) & 6u);
-  const uint32_t bad = classify_tile<false>(t, sh, tid, at, false, parts);
+  const uint32_t parts = (note >> 2) & 6u;  // the halos (rare): classify_tile's lanes
+  if (parts) (void)classify_tile<false>(t, sh, tid, at, false, parts);
   bk.sync();
-  return ((e >> 1) & 1u ? bad : bad0) | (e & 1u);
+  return bad | (e & 1u);
+}
+
+// The tables every tile reads (byte classes, decoder constants): per tile,
+// or once per workgroup in the persistent form.
+template <class BK>
+DA_HDF void init_tables(Shared &sh, BK &bk) {
+  sh.cls[bk.tid()] = class_of((uint32_t)bk.tid());
+  init_dec_tables(sh.dt, bk);
 }
 
 // MODE 1: count only (size query); MODE 2: parse and write.
-template <int MODE, bool FM = false, class BK>
-DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
+//
+// PERSIST (the kernel's workgroups loop over tiles, svm_fast_tile): `sr`
+// already holds tile k's staged loads and the tables are in place; the tile
+// takes the next tile id from the launch's ticket early on (one returning
+// atomic, its latency hidden behind the tile's work) and issues that tile's
+// loads into `sr` once its own register batch is stored, so the next tile's
+// HBM latency overlaps this tile's stores.  Returns the next tile id (block
+// uniform).  Deadlock-free in any residency: a tile id is handed out only to
+// a resident workgroup, after every lower id was.
+template <int MODE, bool FM = false, bool PERSIST = false, class BK>
+DA_HDF uint32_t tile_p(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k, StageRegs &sr) {
   // Tile k = workgroup k (its blockIdx).  The look-back needs every tile's
   // predecessors to become resident eventually; workgroups are dispatched in
   // index order on every XCD, so the least unstarted tile's XCD only holds
@@ -858,7 +944,7 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
   // capped the 131k-tile launch at ~1.5 ms.)  Should a predecessor ever not
   // publish, kSpinLimit bounds the wait and the exact kernels take over.
   const int tid = bk.tid();
-  if (a.skip_if_gated && *a.gate) return;  // fill phase after an exact-path count: block-uniform
+  if (!PERSIST && a.skip_if_gated && *a.gate) return a.ntiles;  // fill phase after an exact-path count: block-uniform
   FAST_STAMP(k, 0);
   FAST_STAMP(k, 1);
   Tile t;
@@ -866,8 +952,9 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
   t.sh = &sh;
   t.tlo = (uint64_t)k * kTile;
   t.thi = mn<uint64_t>(t.tlo + kTile, a.n);
-  StageRegs sr;
-  stage_issue(a.text, a.n, t.tlo, sr, bk);  // text loads first: the chunk search overlaps them
+  uint32_t knext = a.ntiles;  // thread 0: the ticket's answer (PERSIST)
+  if (PERSIST && tid == 0) knext = gridDim_x() + atomic_add_u32(a.ticket, 1u);
+  if (!PERSIST) stage_issue(a.text, a.n, t.tlo, sr, bk);  // text loads first: the chunk search overlaps them
   ChunkProbe cp;  // wave 0: the window load stays in flight through classification
   if (tid < kWave) cp = chunk_list_begin(a.cs, a.nchunk, t.tlo, bk);
   FAST_STAMP(k, 11);
@@ -876,14 +963,13 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
     sh.nq = 0;
     sh.hashy = 0;
   }
-  sh.cls[tid] = class_of((uint32_t)tid);
-  init_dec_tables(sh.dt, bk);
+  if (!PERSIST) init_tables(sh, bk);
   stage_commit(a.text, a.n, t.tlo, sr, sh.c, bk);
   bk.sync();
   FAST_STAMP(k, 2);
 #if defined(FSVM_ABL_STOP) && FSVM_ABL_STOP == 0  // timing ablation only: stage
   if (sh.c.text[tid] == 0xAB && sh.c.ncs == 7) a.res[15] = sh.c.cnext;
-  return;
+  return a.ntiles;
 #endif
   // ---- classify: segment tid -> slot tid+1; lanes 0..15 also one word each
   // of the 64 bytes before the tile -> slot 0
@@ -891,7 +977,7 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
   // from global memory before the staged bytes
   auto at = [&](uint64_t p) -> uint32_t {
     if (p >= a.n) return 0u;
-    return p + kPre >= t.tlo ? (uint32_t)sh.c.text[p - t.tlo + kPre] : (uint32_t)a.text[p];
+    return p + kPre >= t.tlo ? (uint32_t)sh.c.text[p - t.tlo + kPre] : gbyte(a.text, p);
   };
   uint32_t bad = classify_tile<FM>(t, sh, tid, at, true, 7u);
   FAST_STAMP(k, 9);
@@ -905,7 +991,7 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
   FAST_STAMP(k, 3);
 #if defined(FSVM_ABL_STOP) && FSVM_ABL_STOP == 1  // timing ablation only: stage + classify
   if (sh.u.m.d[tid + 1] == 0x123456789ull) a.res[15] = sh.u.m.n[tid];
-  return;
+  return a.ntiles;
 #endif
   // ---- roles, counts, eligibility
   SegOut so;
@@ -940,7 +1026,7 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
                  nI = (uint32_t)((totp >> 32) & 0xFFFF), nV = (uint32_t)(totp >> 48);
 #if defined(FSVM_ABL_STOP) && FSVM_ABL_STOP == 2  // + roles + block scan
   if (ex == 0x123456789ull) a.res[15] = totp;
-  return;
+  return a.ntiles;
 #endif
   // ---- publish this tile's aggregate
   const uint32_t cnt4[4] = {nL, nI, nV, nW};  // look-back slots Q_ROWS, Q_INDEX, Q_VALUE, Q_WEIGHT
@@ -1108,11 +1194,13 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
     if (MODE == 2 && k == 1 && tid == 0) atomic_or_u32(a.gate, 2u);
 #endif
   }
+  if (PERSIST && tid == 0) sh.next = knext;
   bk.sync();
   FAST_STAMP(k, 7);
+  const uint32_t kn = PERSIST ? sh.next : a.ntiles;
 #if defined(FSVM_ABL_STOP) && FSVM_ABL_STOP == 3  // + first decode batch + look-back
   if (sh.c.base[0] == 0x123456789ull) a.res[15] = (uint64_t)ib[0] + (uint64_t)fb[0];
-  return;
+  return a.ntiles;
 #endif
   const uint64_t bRows = sh.c.base[Q_ROWS], bIdx = sh.c.base[Q_INDEX], bVal = sh.c.base[Q_VALUE],
                  bW = sh.c.base[Q_WEIGHT];
@@ -1128,7 +1216,10 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
     a.res[C_FIELD] = FM ? bIdx + nI : 0;
     if (MODE == 2 && a.offset && rows < a.cap[C_ROWS] + 1) a.offset[rows] = bIdx + nI;
   }
-  if (MODE != 2) return;
+  if (MODE != 2) {
+    if (PERSIST && kn < a.ntiles) stage_issue(a.text, a.n, (uint64_t)kn * kTile, sr, bk);
+    return kn;
+  }
 
   // ---- stores
   const uint64_t eL = bRows + fL(ex), eW = bW + fW(ex), eI = bIdx + fI(ex), eV = bVal + fV(ex);
@@ -1215,6 +1306,10 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
       if (j < nF0) put_float(j, fb[u], sh.u.lst[fb0 + j], 0, nV0, nL0);
     }
   }
+#ifndef FSVM_PF_LATE
+  // the next tile's text loads, in flight through the rest of this tile
+  if (PERSIST && kn < a.ntiles) stage_issue(a.text, a.n, (uint64_t)kn * kTile, sr, bk);
+#endif
   for (uint32_t p = 0; p < np; ++p) {
     const uint64_t s = p ? sh.pend[p - 1] : 0, e = p ? sh.pend[p] : pe0;
     if (p) {  // block-uniform
@@ -1290,6 +1385,16 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
       row[C_FIELD] = FM ? row[C_INDEX] : 0;
     }
   }
+#ifdef FSVM_PF_LATE
+  if (PERSIST && kn < a.ntiles) stage_issue(a.text, a.n, (uint64_t)kn * kTile, sr, bk);
+#endif
+  return kn;
+}
+
+template <int MODE, bool FM = false, class BK>
+DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
+  StageRegs sr;
+  (void)tile_p<MODE, FM, false>(a, sh, bk, k, sr);
 }
 
 }  // namespace fsvm

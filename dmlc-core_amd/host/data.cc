@@ -150,6 +150,10 @@ class HipRowIter : public dmlc::RowBlockIter<I, D> {
       }
     }
     row_.size = offset_.size() - 1;
+    // fewer weights / qids than rows (libsvm rows without label:weight or
+    // qid:): a reader takes `size` of them, so the tail reads as zeros
+    if (!weight_.empty() && weight_.size() < row_.size) weight_.resize(row_.size, 0.0f);
+    if (!qid_.empty() && qid_.size() < row_.size) qid_.resize(row_.size, 0);
     row_.offset = offset_.data();
     row_.label = dmlc::BeginPtr(label_);
     row_.weight = dmlc::BeginPtr(weight_);
@@ -277,6 +281,12 @@ struct Page {
     CHECK(fi->Read(&value)) << "Bad RowBlock format";
     CHECK(fi->Read(&max_field, sizeof(I)) == sizeof(I)) << "Bad RowBlock format";
     CHECK(fi->Read(&max_index, sizeof(I)) == sizeof(I)) << "Bad RowBlock format";
+    // a page of libsvm blocks where only some rows had label:weight / qid:
+    // holds fewer of them than rows; a RowBlock reader takes `size` of each
+    // (the reference's own pages read past the vector there): pad the
+    // in-memory copy with zeros (the file keeps the reference's bytes)
+    if (!weight.empty() && weight.size() < Size()) weight.resize(Size(), 0.0f);
+    if (!qid.empty() && qid.size() < Size()) qid.resize(Size(), 0);
     return true;
   }
   // GetBlock (row_block.h:171-189) with its CHECKs

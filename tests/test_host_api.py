@@ -407,7 +407,37 @@ def test_api_disk_row_cache_partial_weights_and_qids(tmp_path):
     h = run_api(tmp_path, d + "#" + cache, iter_=True)
     o, _ = oracle_files(contents)
     assert "error" not in h, h
-    assert len(h["weight"]) == len(o["weight"]) == 10000 and len(h["qid"]) == len(o["qid"]) == 6000
-    assert diff(h, o) == []
+    assert len(o["weight"]) == 10000 and len(o["qid"]) == 6000
+    # the page file itself (RowBlockContainer::Save, row_block.h:190-216): each
+    # vector as a u64 count + its elements, then max_field / max_index
+    pages = _cache_pages(cache)
+    assert len(pages) == 1
+    pg = pages[0]
+    assert pg["weight"].tobytes() == np.asarray(o["weight"], np.float32).tobytes()
+    assert pg["qid"].tolist() == np.asarray(o["qid"]).tolist()
+    assert pg["offset"].tolist() == np.asarray(o["offset"]).tolist()
+    assert pg["index"].tolist() == np.asarray(o["index"]).tolist()
+    # iterated back: a RowBlock carries no weight / qid count, so a reader
+    # takes `size` of them (as from the reference's own pages); the rest equal
+    keep = {k: v for k, v in o.items() if k not in ("weight", "qid")}
+    assert diff(h, keep) == []
     again = run_api(tmp_path, d + "#" + cache, iter_=True)  # the cache reused
-    assert diff(again, o) == []
+    assert diff(again, keep) == [] and _cache_pages(cache)[0]["weight"].size == 10000
+
+
+def _cache_pages(path, index_dtype=np.uint32, value_dtype=np.float32):
+    """Pages of a uri#cachefile (RowBlockContainer<uint32_t, real_t>::Save)."""
+    raw = open(path, "rb").read()
+    pos, pages = 0, []
+    spec = (("offset", np.uint64), ("label", value_dtype), ("weight", np.float32), ("qid", np.uint64),
+            ("field", index_dtype), ("index", index_dtype), ("value", value_dtype))
+    while pos < len(raw):
+        pg = {}
+        for name, dt in spec:
+            n = int(np.frombuffer(raw, np.uint64, 1, pos)[0])
+            pos += 8
+            pg[name] = np.frombuffer(raw, dt, n, pos)
+            pos += n * np.dtype(dt).itemsize
+        pos += 2 * np.dtype(index_dtype).itemsize  # max_field, max_index
+        pages.append(pg)
+    return pages
