@@ -46,11 +46,18 @@ CONFIGS = {
     "libsvm_im1_1m_x128": ("libsvm", 1 << 20, 128, None),  # config 2 with ?indexing_mode=-1
     "csv_i32_1m_x256": ("csv", 1 << 20, 256, None),        # config 3 parsed as Parser<uint32_t, int32_t>
     "csv_sp_1m_x256": ("csv_sp", 1 << 20, 256, None),      # config 3 with ", " between values
+    # the exact kernels (the path input outside the single-pass grammar takes:
+    # inf / nan tokens, BOM lines, '#' lines after a range's first line, qid
+    # mixes) on configs 2 / 3, forced with DMLC_AMD_FLAG_EXACT
+    "libsvm_exact_1m_x128": ("libsvm", 1 << 20, 128, None),
+    "csv_exact_1m_x256": ("csv", 1 << 20, 256, None),
 }
 # parser arguments per config (dmlc_amd_params; the reference's URI args)
 PARAMS = {
     "libsvm_im1_1m_x128": {"indexing_mode": -1},
     "csv_i32_1m_x256": {"value_type": "i32"},
+    "libsvm_exact_1m_x128": {"flags": dmlc_amd.FLAG_EXACT},
+    "csv_exact_1m_x256": {"flags": dmlc_amd.FLAG_EXACT},
 }
 DESC = {
     "libsvm_1m_x128": "libsvm 1M rows x 128 nnz/row, device-resident",
@@ -63,6 +70,8 @@ DESC = {
     "libsvm_im1_1m_x128": "libsvm 1M rows x 128 nnz/row, indexing_mode=-1 (per-range 1-based detection), device-resident",
     "csv_i32_1m_x256": "CSV dense 1M rows x 256 cols parsed with DType int32 (strtoll), device-resident",
     "csv_sp_1m_x256": "CSV dense 1M rows x 256 float cols, ', ' separators, device-resident",
+    "libsvm_exact_1m_x128": "libsvm 1M rows x 128 nnz/row on the exact kernels (DMLC_AMD_FLAG_EXACT), device-resident",
+    "csv_exact_1m_x256": "CSV dense 1M rows x 256 float cols on the exact kernels (DMLC_AMD_FLAG_EXACT), device-resident",
 }
 SYNTH = {"libsvm": synth.LIBSVM, "csv": synth.CSV, "libfm": synth.LIBFM, "libsvm_qid": synth.LIBSVM_QID,
          "libsvm_cmt": synth.LIBSVM_CMT, "csv_sp": synth.CSV_SP}

@@ -1,0 +1,59 @@
+"""Host link rates on the GPU box: what the end-to-end pipeline
+can reach.  Page-locked host buffers <-> HBM, 1 GiB each way:
+  * h2d / d2h alone, by copy kernel (dmlc_amd_copy) and by DMA (hipMemcpyAsync)
+  * both directions at once on two streams (the pipeline's steady state:
+    batch k's CSR out while batch k+1's text comes in)
+One JSON line per measurement (best of 3).  Diagnostic only."""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "dmlc-core_amd", "python")]
+import torch  # noqa: E402
+
+import dmlc_amd  # noqa: E402
+
+
+def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 30
+    L = dmlc_amd.lib()
+    host_in = torch.empty(n, dtype=torch.uint8).pin_memory()
+    host_out = torch.empty(n, dtype=torch.uint8).pin_memory()
+    dev_in = torch.empty(n, dtype=torch.uint8, device="cuda")
+    dev_out = torch.ones(n, dtype=torch.uint8, device="cuda")
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+
+    def kcopy(dst, src, s):
+        assert L.dmlc_amd_copy(dst.data_ptr(), src.data_ptr(), n, s.cuda_stream) == 0
+
+    def dcopy(dst, src, s):
+        with torch.cuda.stream(s):
+            dst.copy_(src, non_blocking=True)
+
+    cases = {
+        "h2d_kernel": [(kcopy, dev_in, host_in, s1)],
+        "d2h_kernel": [(kcopy, host_out, dev_out, s1)],
+        "h2d_dma": [(dcopy, dev_in, host_in, s1)],
+        "d2h_dma": [(dcopy, host_out, dev_out, s1)],
+        "both_kernel": [(kcopy, dev_in, host_in, s1), (kcopy, host_out, dev_out, s2)],
+        "both_dma": [(dcopy, dev_in, host_in, s1), (dcopy, host_out, dev_out, s2)],
+        "h2d_kernel_d2h_dma": [(kcopy, dev_in, host_in, s1), (dcopy, host_out, dev_out, s2)],
+    }
+    for name, ops in cases.items():
+        best = 1e30
+        for _ in range(3):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for f, d, s_, st in ops:
+                f(d, s_, st)
+            torch.cuda.synchronize()
+            best = min(best, time.perf_counter() - t0)
+        moved = n * len(ops)
+        print(json.dumps({"case": name, "bytes": moved, "s": round(best, 5), "GBps": round(moved / best / 1e9, 2)}),
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()
