@@ -1344,8 +1344,13 @@ DA_HDF uint32_t tile_p(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k, Sta
     for (uint64_t m = so.Q; m; m &= m - 1) {
       const uint64_t bit = m & (0 - m), x = P + ctz64(m);
       const uint64_t r = eL + popc64(so.L & (bit - 1)) - 1;  // the row of the label before it
+      // 1-18 digits (qid_ok), staged: the 16-byte window unless longer than 15
+      const W16 w = win_at(sh.c.text, t.tlo, x);
+      const uint32_t len = run_len(w.digits(), 0);
       uint64_t v = 0;
-      for (uint64_t q = x; is_digit(at(q)); ++q) v = v * 10 + (at(q) - '0');
+      if (len < 16) v = w.span16(0, len);
+      else
+        for (uint64_t q = x; is_digit(at(q)); ++q) v = v * 10 + (at(q) - '0');
       if (r < a.cap[C_QID]) a.qid[r] = v;
       else raise_error(a.err, E_CAPACITY, x);
     }

@@ -343,7 +343,14 @@ struct EngineConfig {
   int depth = 0;             // parsed batches ahead of the consumer (0: 2 per worker)
   bool max_index = false;    // reduce index/field maxima on the device (RowBlockIter::NumCol)
   bool stats = false;        // DMLC_AMD_STATS=1: per-stage times on stderr when the parser ends
-  bool kernel_copy = true;   // H2D / D2H by dmlc_amd_copy (DMLC_AMD_COPY=dma: hipMemcpyAsync)
+  // H2D / D2H (DMLC_AMD_COPY): "kernel" (default): the text by dmlc_amd_copy,
+  // the batch's CSR arrays by one dmlc_amd_copy_n launch; "dma": one
+  // hipMemcpyAsync per array.  (Measured on the MI355X box, DESIGN.md 5.2:
+  // kernel copies 27 GB/s end to end, DMA 17 GB/s, and DMA with the CSR
+  // gathered on the device into one D2H copy 18 GB/s -- although the SDMA
+  // engines run both directions of 1 GiB copies at 97 GB/s together,
+  // tools/e2e/link_probe.py)
+  enum CopyMode { kKernel, kDma } copy_mode = kKernel;
 
   // batch size, devices and workers from the environment
   // (DMLC_AMD_BATCH_BYTES, DMLC_AMD_DEVICES = "0,1,..." | "all", DMLC_AMD_WORKERS)
@@ -353,8 +360,8 @@ struct EngineConfig {
     if (const char *st = std::getenv("DMLC_AMD_STATS")) stats = std::atoi(st) != 0;
     if (const char *c = std::getenv("DMLC_AMD_COPY")) {
       const std::string v(c);
-      if (v != "dma" && v != "kernel") throw dmlc::Error("DMLC_AMD_COPY: expected dma or kernel, got " + v);
-      kernel_copy = v == "kernel";
+      if (v != "dma" && v != "kernel") throw dmlc::Error("DMLC_AMD_COPY: expected kernel or dma, got " + v);
+      copy_mode = v == "kernel" ? kKernel : kDma;
     }
     if (const char *d = std::getenv("DMLC_AMD_DEVICES")) {
       devices.clear();
@@ -670,16 +677,20 @@ class HipTextParser : public dmlc::Parser<IndexType, DType> {
     } else {
       b->fail_unit = SIZE_MAX;
     }
-    // the CSR into the batch's pinned arrays
-    auto d2h = [&](void *dst, const void *src, size_t bytes) { D2H(dst, src, bytes, s); };
-    d2h(b->off.reserve(c[DMLC_AMD_ROWS] + 1), out.offset, (c[DMLC_AMD_ROWS] + 1) * 8);
-    d2h(b->label.reserve(c[DMLC_AMD_LABEL] + 1), out.label, c[DMLC_AMD_LABEL] * sizeof(DType));
-    d2h(b->weight.reserve(c[DMLC_AMD_WEIGHT] + 1), out.weight, c[DMLC_AMD_WEIGHT] * 4);
-    d2h(b->qid.reserve(c[DMLC_AMD_QID] + 1), out.qid, c[DMLC_AMD_QID] * 8);
-    d2h(b->index.reserve(c[DMLC_AMD_INDEX] + 1), out.index, c[DMLC_AMD_INDEX] * sizeof(IndexType));
-    d2h(b->field.reserve(c[DMLC_AMD_FIELD] + 1), out.field, c[DMLC_AMD_FIELD] * sizeof(IndexType));
-    d2h(b->value.reserve(c[DMLC_AMD_VALUE] + 1), out.value, c[DMLC_AMD_VALUE] * sizeof(DType));
-    d2h(b->tab.reserve(nunits * 8), d_tab, nunits * 64);
+    // the CSR to the host: offsets, labels, weights, qids, indices, fields,
+    // values, unit table
+    const void *src[8] = {out.offset, out.label, out.weight, out.qid, out.index, out.field, out.value, d_tab};
+    const uint64_t nb[8] = {(c[DMLC_AMD_ROWS] + 1) * 8, c[DMLC_AMD_LABEL] * sizeof(DType), c[DMLC_AMD_WEIGHT] * 4,
+                            c[DMLC_AMD_QID] * 8, c[DMLC_AMD_INDEX] * sizeof(IndexType),
+                            c[DMLC_AMD_FIELD] * sizeof(IndexType), c[DMLC_AMD_VALUE] * sizeof(DType),
+                            (uint64_t)nunits * 64};
+    void *dst[8] = {b->off.reserve(c[DMLC_AMD_ROWS] + 1), b->label.reserve(c[DMLC_AMD_LABEL] + 1),
+                    b->weight.reserve(c[DMLC_AMD_WEIGHT] + 1), b->qid.reserve(c[DMLC_AMD_QID] + 1),
+                    b->index.reserve(c[DMLC_AMD_INDEX] + 1), b->field.reserve(c[DMLC_AMD_FIELD] + 1),
+                    b->value.reserve(c[DMLC_AMD_VALUE] + 1), b->tab.reserve(nunits * 8)};
+    if (cfg_.copy_mode == EngineConfig::kKernel) CheckRc(dmlc_amd_copy_n(dst, src, nb, 8, s));
+    else
+      for (int i = 0; i < 8; ++i) D2H(dst[i], src[i], nb[i], s);
     if (st) hip_check(hipEventRecord(w->ev[3], s), "hipEventRecord");
     hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
     const Clock clk;
@@ -696,16 +707,15 @@ class HipTextParser : public dmlc::Parser<IndexType, DType> {
   }
 
   // Bulk copies between the batch's page-locked arrays and HBM: by kernel
-  // (dmlc_amd_copy) unless DMLC_AMD_COPY=dma; one SDMA engine per copy
-  // capped the pipeline
+  // (dmlc_amd_copy) unless DMLC_AMD_COPY=dma
   void H2D(void *dst, const void *src, size_t bytes, hipStream_t s) {
     if (!bytes) return;
-    if (cfg_.kernel_copy) CheckRc(dmlc_amd_copy(dst, src, bytes, s));
+    if (cfg_.copy_mode == EngineConfig::kKernel) CheckRc(dmlc_amd_copy(dst, src, bytes, s));
     else hip_check(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s), "H2D");
   }
   void D2H(void *dst, const void *src, size_t bytes, hipStream_t s) {
     if (!bytes) return;
-    if (cfg_.kernel_copy) CheckRc(dmlc_amd_copy(dst, src, bytes, s));
+    if (cfg_.copy_mode == EngineConfig::kKernel) CheckRc(dmlc_amd_copy(dst, src, bytes, s));
     else hip_check(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s), "D2H");
   }
 

@@ -74,6 +74,10 @@ def lib():
         L.dmlc_amd_last_hip_error.restype = ctypes.c_char_p
         L.dmlc_amd_copy.restype = ctypes.c_int
         L.dmlc_amd_copy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
+        if hasattr(L, "dmlc_amd_copy_n"):  # (absent from older diagnostic variant builds)
+            L.dmlc_amd_copy_n.restype = ctypes.c_int
+            L.dmlc_amd_copy_n.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p),
+                                          ctypes.POINTER(ctypes.c_uint64), ctypes.c_int, ctypes.c_void_p]
         L.dmlc_amd_profile_begin.restype = ctypes.c_int
         L.dmlc_amd_profile_end.restype = ctypes.c_int
         L.dmlc_amd_profile_end.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int),

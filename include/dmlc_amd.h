@@ -147,6 +147,12 @@ int dmlc_amd_strtof_batch(const void *d_text, const uint64_t *d_offsets, uint64_
  * hipMemcpyAsync.  Asynchronous on `stream`. */
 int dmlc_amd_copy(void *dst, const void *src, uint64_t bytes, void *stream);
 
+/* n <= DMLC_AMD_COPY_MAX such copies (dst[i] <- src[i], bytes[i]) in one
+ * kernel launch: the CSR arrays of a parsed batch in one D2H step.  Zero-byte
+ * entries are skipped; a pair not 16-byte aligned is copied on its own. */
+#define DMLC_AMD_COPY_MAX 16
+int dmlc_amd_copy_n(void *const *dst, const void *const *src, const uint64_t *bytes, int n, void *stream);
+
 /* Kernel timing for benchmarks: between profile_begin and profile_end, every
  * dmlc_amd_parse on this thread brackets its dominant kernel (the single-pass
  * kernel, or the exact write kernel) with HIP events on its stream.

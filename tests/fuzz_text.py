@@ -73,13 +73,15 @@ def uniform_libsvm(rng, nlines, maxfeat=40, violate=False):
     return text.encode("latin-1")
 
 
-def qid_libsvm(rng, nlines, maxfeat=40, violate=False, mixed=False):
+def qid_libsvm(rng, nlines, maxfeat=40, violate=False, mixed=False, long_head=False):
     """libsvm ranking rows, "<label>[:<weight>] qid:<n> <idx>:<val> ...", in the
     fast grammar (svm_fast.h qid_clean / qid_ok): the token after the label
     (any blanks) or after label:weight (spaces), 1-18 digits.  violate=True
     mixes in the forms the reference reads differently (a tab after the
     weight, "qid: 5", "qid:5.5", a second token, a token among the features,
-    19 digits, stray letters); mixed=True leaves some rows without a qid."""
+    19 digits, stray letters); mixed=True leaves some rows without a qid;
+    long_head=True makes some line heads longer than 64 bytes (long labels and
+    weights, long blank runs before the token)."""
     out = []
     for _ in range(nlines):
         if rng.random() < 0.03:
@@ -91,6 +93,15 @@ def qid_libsvm(rng, nlines, maxfeat=40, violate=False, mixed=False):
             parts.append(rng.choice([":", " :", ": "]) + _num(rng))
         q = str(int(rng.integers(0, 10 ** int(rng.integers(1, 19)))))
         sep = rng.choice([" ", "  ", " ", ""] if wt else [" ", "\t", "  ", " \t", ""])
+        if long_head and rng.random() < 0.4:
+            k = int(rng.integers(30, 90))
+            pick = int(rng.integers(0, 3))
+            if pick == 0:
+                sep = " " * k if wt else rng.choice([" " * k, "\t" * (k // 3) + " "])
+            elif pick == 1:
+                parts[0] = parts[0] + "0" * k if "." in parts[0] else parts[0] + "." + "1" * k
+            elif wt:
+                parts[-1] = parts[-1] + "5" * k if "." in parts[-1] else parts[-1] + ".0" + "7" * k
         tok = sep + "qid:" + q
         if violate and rng.random() < 0.15:
             tok = rng.choice(["\tqid:" + q if wt else " qid: " + q, " qid:5.5", " qid:-3", " qid:", " qid:5:3",

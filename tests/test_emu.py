@@ -189,6 +189,21 @@ def test_emu_fast_qid_vs_oracle():
     assert paths["fast"] >= 20 and paths["exact"] >= 5, paths
 
 
+def test_emu_fast_qid_long_heads_vs_oracle():
+    """qid runs whose line head (label, weight, blanks before the token) is
+    longer than the tile's 64-byte pre-halo or crosses a tile start
+    (svm_fast.h Tile::qid_ok reads the staged text only), tabs among long
+    blanks."""
+    rng = np.random.default_rng(4343)
+    fast = 0
+    for it in range(24):
+        data = fuzz_text.qid_libsvm(rng, int(rng.integers(5, 60)), 10, violate=it % 6 == 5, long_head=True)
+        offs = fuzz_text.random_cuts(rng, data, 4, anywhere=it % 4 == 3)
+        h = _emu_vs_oracle(data, offs, **({"index_bits": 64} if it % 3 == 1 else {}))
+        fast += h["path"] == "fast"
+    assert fast >= 8, fast
+
+
 def test_emu_libfm_dense_runs():
     """libfm tiles of one-byte runs: index, field and value lists in passes."""
     rng = np.random.default_rng(93)

@@ -719,6 +719,31 @@ def test_gpu_kernel_copy_host_device(dm, nbytes, shift):
     assert torch.equal(back[shift:], src[shift:])
 
 
+def test_gpu_kernel_copy_n(dm):
+    """dmlc_amd_copy_n (the engine's D2H of a batch's CSR arrays in one
+    launch): every pair byte for byte, odd sizes (tails), empty entries
+    skipped, an unaligned pair on its own, nothing written past an end."""
+    import ctypes
+    import torch
+    L = dm.lib()
+    rng = np.random.default_rng(5)
+    sizes = [8 * 300001, 0, 13, 4 * 2_000_003, 4096, 1 << 20, 7, 64 * 1001]
+    srcs = [torch.from_numpy(rng.integers(0, 256, n + 32, dtype=np.uint8)).cuda() for n in sizes]
+    dsts = [torch.zeros(n + 32, dtype=torch.uint8).pin_memory() for n in sizes]
+    shift = [0] * len(sizes)
+    shift[6] = 3  # unaligned host side
+    dp = (ctypes.c_void_p * len(sizes))(*[d.data_ptr() + h for d, h in zip(dsts, shift)])
+    sp = (ctypes.c_void_p * len(sizes))(*[x.data_ptr() for x in srcs])
+    nb = (ctypes.c_uint64 * len(sizes))(*sizes)
+    s = torch.cuda.current_stream().cuda_stream
+    assert L.dmlc_amd_copy_n(dp, sp, nb, len(sizes), s) == 0
+    torch.cuda.synchronize()
+    for n, h, x, d in zip(sizes, shift, srcs, dsts):
+        assert torch.equal(d[h:h + n], x[:n].cpu()), n
+        assert int(d[h + n:].sum()) == 0 and int(d[:h].sum()) == 0, n
+    assert L.dmlc_amd_copy_n(dp, sp, nb, 17, s) != 0  # more than DMLC_AMD_COPY_MAX
+
+
 @pytest.mark.parametrize("fmt", [po.LIBSVM, po.LIBFM])
 def test_gpu_qid_letter_forms_vs_oracle(dm, fmt):
     """Letters of "qid" that spell no "qid:" token leave the single-pass

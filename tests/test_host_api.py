@@ -391,6 +391,34 @@ def test_api_multi_device_dispatch(tmp_path):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["kernel", "dma"])
+def test_api_copy_modes(tmp_path, mode):
+    """DMLC_AMD_COPY: the batch's CSR arrays copied out by one copy kernel
+    (kernel, the default) or one DMA per array (dma) -- both modes' blocks
+    equal the oracle's parse, over many
+    batches, with weights and qids and a CSV / libfm file."""
+    text, _ = synth.rows(synth.LIBSVM, 30000, 48, seed=21)
+    lines = text.tobytes().split(b"\n")
+    for i in range(0, len(lines) - 1):  # label:weight and qid on every row (a RowBlock reader takes `size`)
+        head, _, rest = lines[i].partition(b" ")
+        lines[i] = head + b":0.%d qid:%d " % (1 + i % 9, i // 3) + rest
+    svm = b"\n".join(lines)
+    env = {"DMLC_AMD_COPY": mode, "DMLC_AMD_BATCH_BYTES": str(1 << 20)}
+    d, _ = _write(tmp_path / "svm", [svm])
+    o, _ = oracle_files([svm])
+    h = run_api(tmp_path, d, env=env)
+    assert "error" not in h and diff(h, o) == [], mode
+    assert h["blocks"].tolist() == o["blocks"]["rows"].tolist(), mode
+    for fmt, pfmt in ((synth.CSV, po.CSV), (synth.LIBFM, po.LIBFM)):
+        t, _ = synth.rows(fmt, 20000, 24, seed=22)
+        name = {po.CSV: "csv", po.LIBFM: "libfm"}[pfmt]
+        dd, _ = _write(tmp_path / name, [t.tobytes()])
+        oo, _ = oracle_files([t.tobytes()], fmt=pfmt)
+        hh = run_api(tmp_path, dd, fmt=name, env=env)
+        assert "error" not in hh and diff(hh, oo) == [], (mode, name)
+
+
+@pytest.mark.gpu
 def test_api_disk_row_cache_partial_weights_and_qids(tmp_path):
     """uri#cachefile over libsvm blocks where only some rows carry label:weight
     or qid: (fewer weights / qids than rows in a block): the cache pages hold

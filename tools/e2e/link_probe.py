@@ -55,5 +55,24 @@ def main():
               flush=True)
 
 
+def host_memcpy(n=1 << 30, threads=(1, 4, 8, 16)):
+    """Host DRAM copy rate (what the reader's page-cache -> pinned copy and the
+    links' DMA share): (read + write bytes) / time, best of 3."""
+    import concurrent.futures
+    import numpy as np
+    a = np.ones(n, dtype=np.uint8)
+    b = np.empty_like(a)
+    for t in threads:
+        step = n // t
+        best = 1e30
+        with concurrent.futures.ThreadPoolExecutor(t) as ex:
+            for _ in range(3):
+                t0 = time.perf_counter()
+                list(ex.map(lambda i: np.copyto(b[i * step:(i + 1) * step], a[i * step:(i + 1) * step]), range(t)))
+                best = min(best, time.perf_counter() - t0)
+        print(json.dumps({"case": "host_memcpy", "threads": t, "GBps_rw": round(2 * n / best / 1e9, 1)}), flush=True)
+
+
 if __name__ == "__main__":
     main()
+    host_memcpy()

@@ -1,13 +1,13 @@
 #!/bin/bash
 # End-to-end engine knob sweep on the GPU box (copy mode x workers per device
 # x batch bytes), libsvm config 2 by default: one JSON line per setting on stdout.
-#   [MODES="packed kernel dma"] [WORKERS="2 3 4"] [BATCHES=...] [CONFIGS=...] bash tools/e2e_sweep.sh
+#   [MODES="kernel dma"] [WORKERS="2 3 4"] [BATCHES=...] [CONFIGS=...] bash tools/e2e_sweep.sh
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out; mkdir -p $O
 cd $R
 export TMPDIR=${TMPDIR:-/tmp}
-for m in ${MODES:-packed}; do
+for m in ${MODES:-kernel}; do
 for w in ${WORKERS:-2 3 4}; do
   for b in ${BATCHES:-33554432 67108864}; do
     t=${m}_w${w}_b${b}
