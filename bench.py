@@ -44,6 +44,7 @@ CONFIGS = {
     # grammar variants of configs 2 / 3 (the rates real data hits
     # off the canonical shape)
     "libsvm_im1_1m_x128": ("libsvm", 1 << 20, 128, None),  # config 2 with ?indexing_mode=-1
+    "libsvm_1b_im1_1m_x128": ("libsvm_1b", 1 << 20, 128, None),  # 1-based ids, ?indexing_mode=-1 (every id shifted)
     "csv_i32_1m_x256": ("csv", 1 << 20, 256, None),        # config 3 parsed as Parser<uint32_t, int32_t>
     "csv_sp_1m_x256": ("csv_sp", 1 << 20, 256, None),      # config 3 with ", " between values
     # the exact kernels (the path input outside the single-pass grammar takes:
@@ -55,6 +56,7 @@ CONFIGS = {
 # parser arguments per config (dmlc_amd_params; the reference's URI args)
 PARAMS = {
     "libsvm_im1_1m_x128": {"indexing_mode": -1},
+    "libsvm_1b_im1_1m_x128": {"indexing_mode": -1},
     "csv_i32_1m_x256": {"value_type": "i32"},
     "libsvm_exact_1m_x128": {"flags": dmlc_amd.FLAG_EXACT},
     "csv_exact_1m_x256": {"flags": dmlc_amd.FLAG_EXACT},
@@ -68,16 +70,18 @@ DESC = {
     "libsvm_qid_1m_x128": "libsvm 1M rows x 128 nnz/row with qid:<row/16> on every row, device-resident",
     "libsvm_cmt_1m_x128": "libsvm 1M rows x 128 nnz/row, a '# row <r>' comment on every row and a header, device-resident",
     "libsvm_im1_1m_x128": "libsvm 1M rows x 128 nnz/row, indexing_mode=-1 (per-range 1-based detection), device-resident",
+    "libsvm_1b_im1_1m_x128": "libsvm 1M rows x 128 nnz/row with 1-based ids, indexing_mode=-1 (every range detected 1-based and shifted), device-resident",
     "csv_i32_1m_x256": "CSV dense 1M rows x 256 cols parsed with DType int32 (strtoll), device-resident",
     "csv_sp_1m_x256": "CSV dense 1M rows x 256 float cols, ', ' separators, device-resident",
     "libsvm_exact_1m_x128": "libsvm 1M rows x 128 nnz/row on the exact kernels (DMLC_AMD_FLAG_EXACT), device-resident",
     "csv_exact_1m_x256": "CSV dense 1M rows x 256 float cols on the exact kernels (DMLC_AMD_FLAG_EXACT), device-resident",
 }
 SYNTH = {"libsvm": synth.LIBSVM, "csv": synth.CSV, "libfm": synth.LIBFM, "libsvm_qid": synth.LIBSVM_QID,
-         "libsvm_cmt": synth.LIBSVM_CMT, "csv_sp": synth.CSV_SP}
+         "libsvm_cmt": synth.LIBSVM_CMT, "csv_sp": synth.CSV_SP, "libsvm_1b": synth.LIBSVM_1B}
 # the arithmetic the path computes in (values decoded to f32 through the
 # reference's f64 fraction divide; indices / fields as u32)
-DTYPE = {"libsvm": "f32 values / u32 index", "libsvm_qid": "f32 values / u32 index / u64 qid",
+DTYPE = {"libsvm": "f32 values / u32 index", "libsvm_1b": "f32 values / u32 index",
+         "libsvm_qid": "f32 values / u32 index / u64 qid",
          "libsvm_cmt": "f32 values / u32 index",
          "csv": "f32 values", "csv_sp": "f32 values", "libfm": "f32 values / u32 index / u32 field"}
 
@@ -223,7 +227,7 @@ def main():
     d_text = torch.from_numpy(text).to(dev)
     d_starts = torch.from_numpy(starts).to(dev)
     nbytes = int(text.size)
-    pfmt = {"libsvm_qid": "libsvm", "libsvm_cmt": "libsvm", "csv_sp": "csv"}.get(fmt, fmt)
+    pfmt = {"libsvm_qid": "libsvm", "libsvm_cmt": "libsvm", "libsvm_1b": "libsvm", "csv_sp": "csv"}.get(fmt, fmt)
     pkw = dict(PARAMS.get(args.config, {}))
     if pfmt == "csv":
         pkw["label_column"] = args.label_column

@@ -93,7 +93,7 @@ struct MinAcc {
     }
   }
   DA_HD void flush(uint64_t *cmin) {
-    if (unit >= 0) atomic_min_u64((unsigned long long *)&cmin[unit], (unsigned long long)v);
+    if (unit >= 0) atomic_min_u64_if_lower((unsigned long long *)&cmin[unit], (unsigned long long)v);
     unit = -1;
     v = ~0ull;
   }
@@ -104,7 +104,7 @@ template <class BK>
 DA_HDF void tile_min_flush(MinAcc &m, uint64_t *cmin, BK &bk) {
   const uint64_t u0 = bk.min_u64(m.unit >= 0 ? (uint64_t)m.unit : ~0ull);
   const uint64_t m0 = bk.min_u64(m.unit >= 0 && (uint64_t)m.unit == u0 ? m.v : ~0ull);
-  if (bk.tid() == 0 && u0 != ~0ull) atomic_min_u64((unsigned long long *)&cmin[u0], (unsigned long long)m0);
+  if (bk.tid() == 0 && u0 != ~0ull) atomic_min_u64_if_lower((unsigned long long *)&cmin[u0], (unsigned long long)m0);
   if (m.unit >= 0 && (uint64_t)m.unit != u0) m.flush(cmin);
   m.unit = -1;
 }

@@ -61,6 +61,19 @@ DA_HD void atomic_min_u64(unsigned long long *p, unsigned long long v) {
 #endif
 }
 
+// atomic min, skipped when a plain read already shows a value <= v: minima
+// of many tiles on one word (a ParseBlock unit's) mostly do not improve it,
+// and same-address device atomics serialise (a stale read only costs an
+// atomic: the word only ever decreases)
+DA_HD void atomic_min_u64_if_lower(unsigned long long *p, unsigned long long v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const unsigned long long cur = *(volatile unsigned long long *)p;
+#else
+  const unsigned long long cur = __atomic_load_n(p, __ATOMIC_RELAXED);
+#endif
+  if (v < cur) atomic_min_u64(p, v);
+}
+
 // a text byte from global memory, typed as such: a read that may come from
 // LDS or global memory (the fast kernels' at()) would otherwise become one
 // flat load of a selected pointer, which waits on both counters
@@ -69,6 +82,16 @@ DA_HD uint32_t gbyte(const uint8_t *t, uint64_t p) {
   return *((const __attribute__((address_space(1))) uint8_t *)t + p);
 #else
   return t[p];
+#endif
+}
+
+// a plain store other threads may race with on the same value (a flag);
+// relaxed-atomic on the host so the emulator's threads do not race
+DA_HD void store_flag_u64(uint64_t *p, uint64_t v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  *p = v;
+#else
+  __atomic_store_n(p, v, __ATOMIC_RELAXED);
 #endif
 }
 

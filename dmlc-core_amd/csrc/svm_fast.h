@@ -47,10 +47,10 @@ DA_HD bool qid_decide(uint64_t total, uint64_t *res, uint32_t *gate) {
 }
 
 // ---- indexing_mode < 0 (libsvm_parser.h:165-171; libfm_parser.h:133-143)
-// on the single-pass path: the write pass stores the ids as read and notes
-// each ParseBlock unit's minimum stored id (umin, libfm: over fields and
-// indices); afterwards every id of a unit holding ids, all of them > 0, drops
-// by one.  The units' index ranges are the chunk table's index column (tab,
+// on the single-pass path: the write pass stores the ids as read and marks
+// each ParseBlock unit holding a 0 id (umin[u] = 0, libfm: among fields and
+// indices; ~0 otherwise); afterwards every id of a unit without a 0 id (its
+// minimum is > 0) drops by one.  The units' index ranges are the chunk table's index column (tab,
 // nunit rows of 8, complete after chunk_fixup_kernel).  Entries [lo, hi) of
 // the index array (and the field array, when set), stride `step` from lo.
 DA_HD int unit_of_entry(const uint64_t *tab, int nunit, uint64_t i) {  // last unit whose range starts <= i
@@ -69,8 +69,7 @@ DA_HD void umin_fix(void *index, void *field, int wide, const uint64_t *tab, int
     const uint64_t ulo = tab[(uint64_t)u * 8 + C_INDEX];
     if (ulo >= hi) break;
     const uint64_t uhi = u + 1 < nunit ? tab[(uint64_t)(u + 1) * 8 + C_INDEX] : total;
-    const uint64_t m = umin[u];
-    if (m == ~0ull || m == 0) continue;  // no ids, or a 0 among them: kept
+    if (umin[u] == 0) continue;  // a 0 among the unit's ids: kept (a unit without ids has an empty range)
     const uint64_t a = ulo > lo ? ulo : lo, b = uhi < hi ? uhi : hi;
     for (uint64_t i = a + first; i < b; i += step) {
       if (wide) {
@@ -94,20 +93,25 @@ DA_HD void umin_fix(void *index, void *field, int wide, const uint64_t *tab, int
 // by a digit (atoll's digits).
 DA_HD bool is_qid_letter(uint32_t b) { return b == 'q' || b == 'i' || b == 'd'; }
 // (inline: out of line, the call's stack frame cost the kernel 2.3x)
-template <class At>
-DA_HD bool qid_clean(uint64_t P, uint64_t *n, uint64_t *c, bool lead, At at) {
+// Each run of letters is checked once, at its first letter: the token it
+// must belong to starts where that letter's place in "qid" puts it, and the
+// four bytes there (one word read, `wd`) must be "qid:" -- which also bounds
+// the run to the token's three letters.  (Round 2 read five bytes per letter.)
+constexpr uint32_t kQidWord = 0x3A646971u;  // "qid:" little-endian
+template <class At, class Wd>
+DA_HD bool qid_clean(uint64_t P, uint64_t *n, uint64_t *c, bool lead, At at, Wd wd) {
   const uint64_t X = *n & *c;
   bool ok = true;
-  for (uint64_t m = X; m; m &= m - 1) {
+  for (uint64_t m = X & ~(X << 1); m; m &= m - 1) {
     const uint64_t x = P + ctz64(m);
     const uint32_t b = at(x);
     const uint64_t s0 = x - (b == 'q' ? 0u : b == 'i' ? 1u : 2u);
-    ok = ok && at(s0) == 'q' && at(s0 + 1) == 'i' && at(s0 + 2) == 'd' && at(s0 + 3) == ':';
+    ok = ok && wd(s0) == kQidWord;
   }
   uint64_t qc = 0;
   for (uint64_t m = *c & ~X & ((X << 1) | (lead ? 1u : 0u)); m; m &= m - 1) {
     const uint64_t x = P + ctz64(m);
-    if (at(x - 1) == 'd' && at(x - 2) == 'i' && at(x - 3) == 'q') {
+    if (x >= 3 && wd(x - 3) == kQidWord) {
       qc |= m & (0 - m);
       ok = ok && is_digit(at(x + 1));
     }
@@ -829,12 +833,27 @@ FSVM_COLD bool slow_uint(const uint8_t *text, uint64_t q, uint64_t lim, int wide
 // flag.  `first`: pass 0, which also notes bytes outside the grammar.
 // Segment seg's masks m (classify64_lut's form) into the planes and the
 // digit-plane words, "qid:" tokens cleaned; returns its grammar flag.
+// The four text bytes at p as a little-endian word (0 past the text): two
+// aligned LDS words when staged, else byte by byte through `at`.
+template <class At>
+DA_HD uint32_t text_word(const Tile &t, uint64_t p, At at) {
+  if (p + kPre >= t.tlo && p + 4 <= t.a->n) {
+    const uint64_t off = p + kPre - t.tlo;
+    if (off + 8 <= (uint64_t)kStage) {
+      const uint32_t *w = reinterpret_cast<const uint32_t *>(t.sh->c.text + (off & ~3ull));
+      return funnel(w[1], w[0], (uint32_t)(off & 3u) * 8u);
+    }
+  }
+  return at(p) | (at(p + 1) << 8) | (at(p + 2) << 16) | (at(p + 3) << 24);
+}
+
 template <bool FM, class At>
 DA_HDF uint32_t commit_seg(const Tile &t, Shared &sh, int seg, At at, bool first, Masks m) {
   uint32_t bad = 0;
   const uint64_t P0 = t.tlo + (uint64_t)seg * kSegB;
   if ((m.n & m.c) || ((m.c & 1) && P0 > 0 && is_qid_letter(at(P0 - 1)))) {  // letters: "qid:" tokens
-    if (FM || !qid_clean(P0, &m.n, &m.c, P0 > 0 && is_qid_letter(at(P0 - 1)), at)) bad = 1;
+    auto wd = [&](uint64_t p) -> uint32_t { return text_word(t, p, at); };
+    if (FM || !qid_clean(P0, &m.n, &m.c, P0 > 0 && is_qid_letter(at(P0 - 1)), at, wd)) bad = 1;
   }
   sh.gw[2 * seg] = (uint32_t)m.g;
   sh.gw[2 * seg + 1] = (uint32_t)(m.g >> 32);
@@ -869,7 +888,8 @@ DA_HDF uint32_t classify_tile(const Tile &t, Shared &sh, int tid, At at, bool fi
     const uint64_t P0 = t.tlo - kSegB + 4 * tid;
     if (!FM && ((bn & bc) || (bc & 1))) {  // the bytes' owner tile checks them; here only their planes
       const bool lead = is_qid_letter(at(P0 - 1));
-      if ((bn & bc) || lead) (void)qid_clean(P0, &bn, &bc, lead, at);
+      auto wd = [&](uint64_t p) -> uint32_t { return text_word(t, p, at); };
+      if ((bn & bc) || lead) (void)qid_clean(P0, &bn, &bc, lead, at, wd);
     }
     atomic_or_u64(&sh.u.m.d[0], (uint64_t)b.d << (4 * tid));
     atomic_or_u64(&sh.u.m.n[0], bn << (4 * tid));
@@ -1223,18 +1243,22 @@ DA_HDF uint32_t tile_p(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k, Sta
 
   // ---- stores
   const uint64_t eL = bRows + fL(ex), eW = bW + fW(ex), eI = bIdx + fI(ex), eV = bVal + fV(ex);
-  // indexing_mode < 0: the minimum stored id of each unit (umin_fix): in a
-  // register when the tile lies inside one unit, else a device atomic per id
+  // indexing_mode < 0 (umin_fix): whether a unit holds a 0 id -- all the
+  // reference's rule needs (min_index > 0 <=> no id is 0).  A 0 id marks its
+  // unit's word with a plain store of 0 (in a register first when the tile
+  // lies inside one unit): no atomics, which on one word per unit serialise
+  // (a wave minimum by atomicMin on every tile cost config 2 4.7x)
   const bool imin = a.indexing_mode < 0;
-  uint64_t tmin = ~0ull;
+  bool zero = false;
   auto note_min = [&](uint64_t q, uint64_t v) {
     const uint64_t sv = a.wide ? v : (uint64_t)(uint32_t)v;
+    if (sv != 0) return;
     if (one_chunk) {
-      tmin = sv < tmin ? sv : tmin;
+      zero = true;
     } else {
       uint32_t u = sh.c.c_first - 1;
       for (uint32_t i = 0; i < sh.c.ncs; ++i) u += sh.c.csl[i] <= q ? 1u : 0u;
-      atomic_min_u64((unsigned long long *)&a.umin[u], (unsigned long long)sv);
+      store_flag_u64(&a.umin[u], 0);
     }
   };
   auto put_index = [&](uint64_t r, uint64_t v, uint64_t q) {
@@ -1362,15 +1386,9 @@ DA_HDF uint32_t tile_p(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k, Sta
       if (sh.c.text[q - t.tlo + kPre] == '-') raise_error(a.err, E_NEG_INDEX, q);
     }
   }
-  if (imin && one_chunk) {  // block-uniform: one atomic per wave for the tile's unit
-    uint64_t m = tmin;
-#pragma unroll
-    for (int d = 1; d < kWave; d <<= 1) {
-      const uint64_t o = bk.shfl(m, (int)((uint32_t)(tid ^ d) & (kWave - 1)));
-      m = o < m ? o : m;
-    }
-    if ((tid & (kWave - 1)) == 0 && m != ~0ull)
-      atomic_min_u64((unsigned long long *)&a.umin[sh.c.c_first - 1], (unsigned long long)m);
+  if (imin && one_chunk) {  // block-uniform: one store per wave that saw a 0 id
+    const uint64_t zm = bk.ballot(zero);
+    if ((tid & (kWave - 1)) == 0 && zm) store_flag_u64(&a.umin[sh.c.c_first - 1], 0);
   }
   FAST_STAMP(k, 8);
   // ---- per-chunk exclusive counts at each chunk start in my segment
@@ -1417,13 +1435,44 @@ __global__ void __launch_bounds__(256) umin_fix_kernel(void *index, void *field,
   if (threadIdx.x == 0) need = 0;
   __syncthreads();
   for (int u = threadIdx.x; u < nunit; u += 256)
-    if (umin[u] != ~0ull && umin[u] > 0) need = 1;
+    if (umin[u] != 0) need = 1;
   __syncthreads();
   if (!need) return;
   const uint64_t total = res[C_INDEX];
-  for (uint64_t b = (uint64_t)blockIdx.x * 4096; b < total; b += (uint64_t)gridDim.x * 4096)
-    fsvm::umin_fix(index, field, wide, tab, nunit, umin, total, b, b + 4096 < total ? b + 4096 : total,
-                   threadIdx.x, 256);
+  // a block of 4096 ids inside one unit to shift (the common case: units are
+  // InputSplit chunks or their ranges): 16-byte loads, all in flight before
+  // the stores; a block across a unit start, 64-bit ids or an unaligned
+  // array take the element loop
+  const bool vec = !wide && !field && ((uintptr_t)index & 15u) == 0;
+  __shared__ int blk_u;
+  for (uint64_t b = (uint64_t)blockIdx.x * 4096; b < total; b += (uint64_t)gridDim.x * 4096) {
+    const uint64_t e = b + 4096 < total ? b + 4096 : total;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const int u = fsvm::unit_of_entry(tab, nunit, b);
+      const uint64_t uhi = u + 1 < nunit ? tab[(uint64_t)(u + 1) * 8 + C_INDEX] : total;
+      blk_u = (vec && e == b + 4096 && uhi >= e) ? u : -1;
+    }
+    __syncthreads();
+    const int u = blk_u;
+    if (u < 0) {
+      fsvm::umin_fix(index, field, wide, tab, nunit, umin, total, b, e, threadIdx.x, 256);
+      continue;
+    }
+    if (umin[u] == 0) continue;  // a 0 among the unit's ids: kept
+    uint4 *p = reinterpret_cast<uint4 *>(static_cast<uint32_t *>(index) + b);
+    uint4 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = p[threadIdx.x + 256 * k];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      v[k].x -= 1u;
+      v[k].y -= 1u;
+      v[k].z -= 1u;
+      v[k].w -= 1u;
+      p[threadIdx.x + 256 * k] = v[k];
+    }
+  }
 }
 inline hipError_t launch_umin_fix(void *index, void *field, int wide, const uint64_t *tab, int nunit,
                                   const uint64_t *umin, const uint64_t *res, const uint32_t *gate,

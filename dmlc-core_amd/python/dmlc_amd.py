@@ -101,7 +101,7 @@ def profile_end():
 EXPORTED_SYMBOLS = ("dmlc_amd_parse", "dmlc_amd_workspace_bytes", "dmlc_amd_error_string",
                     "dmlc_amd_device_count", "dmlc_amd_abi_version", "dmlc_amd_strtof_batch",
                     "dmlc_amd_profile_begin", "dmlc_amd_profile_end", "dmlc_amd_last_hip_error",
-                    "dmlc_amd_copy")
+                    "dmlc_amd_copy", "dmlc_amd_copy_n")
 
 
 def make_params(fmt="libsvm", index_bits=32, value_type="f32", indexing_mode=0, label_column=-1,

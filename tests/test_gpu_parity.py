@@ -820,6 +820,23 @@ def test_gpu_csv_variant_bench_configs_fast(dm):
             assert torch.equal(outs[False][k], outs[True][k]), (fmt, vt, k)
 
 
+def test_gpu_indexing_mode_auto_one_based_bench_shape(dm):
+    """indexing_mode=-1 at bench shape (bench.py libsvm_1b_im1_1m_x128): the
+    1-based rows (tools/synth.c fmt 6, every id of config 2 one higher) hold
+    no 0 id in any unit, so every id drops by one -- the result equals the
+    0-based rows parsed as they are (nthread 1 and 2, 8 MiB chunks)."""
+    text1, _ = synth.rows(synth.LIBSVM_1B, 120000, 128, seed=3)
+    text0, _ = synth.rows(synth.LIBSVM, 120000, 128, seed=3)
+    for nthread in (1, 2):
+        offs1 = dm.text_chunk_starts(text1).tolist()
+        offs0 = dm.text_chunk_starts(text0).tolist()
+        h1 = gpu_parse(dm, text1.tobytes(), offs1, indexing_mode=-1, nthread=nthread)
+        h0 = gpu_parse(dm, text0.tobytes(), offs0, nthread=nthread)
+        assert h1["path"] == "fast" and not h1["failed"] and not h0["failed"]
+        for k in ("offset", "label", "index", "value"):
+            assert np.asarray(h1[k]).tobytes() == np.asarray(h0[k]).tobytes(), (nthread, k)
+
+
 @pytest.mark.parametrize("nthread", [1, 2])
 def test_gpu_fast_indexing_mode_auto_vs_oracle(dm, nthread):
     """indexing_mode=-1 on the single-pass libsvm / libfm kernels: each

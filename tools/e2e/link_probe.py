@@ -40,6 +40,7 @@ def main():
         "both_kernel": [(kcopy, dev_in, host_in, s1), (kcopy, host_out, dev_out, s2)],
         "both_dma": [(dcopy, dev_in, host_in, s1), (dcopy, host_out, dev_out, s2)],
         "h2d_kernel_d2h_dma": [(kcopy, dev_in, host_in, s1), (dcopy, host_out, dev_out, s2)],
+        "h2d_dma_d2h_kernel": [(dcopy, dev_in, host_in, s1), (kcopy, host_out, dev_out, s2)],
     }
     for name, ops in cases.items():
         best = 1e30
@@ -52,6 +53,40 @@ def main():
             best = min(best, time.perf_counter() - t0)
         moved = n * len(ops)
         print(json.dumps({"case": name, "bytes": moved, "s": round(best, 5), "GBps": round(moved / best / 1e9, 2)}),
+              flush=True)
+
+
+def batched(nb=40 << 20, reps=24):
+    """The pipeline's shape: reps batches of nb bytes in, nb/2 out, two
+    workers (streams) each copying its batch in, then its CSR out; by copy
+    kernel and by DMA.  GB/s of input moved."""
+    L = dmlc_amd.lib()
+    h_in = [torch.empty(nb, dtype=torch.uint8).pin_memory() for _ in range(2)]
+    h_out = [torch.empty(nb // 2, dtype=torch.uint8).pin_memory() for _ in range(2)]
+    d_in = [torch.empty(nb, dtype=torch.uint8, device="cuda") for _ in range(2)]
+    d_out = [torch.ones(nb // 2, dtype=torch.uint8, device="cuda") for _ in range(2)]
+    ss = [torch.cuda.Stream(), torch.cuda.Stream()]
+    for mode in ("kernel", "dma", "dma_in_kernel_out"):
+        best = 1e30
+        for _ in range(2):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for r in range(reps):
+                w = r % 2
+                s = ss[w]
+                if mode == "kernel":
+                    assert L.dmlc_amd_copy(d_in[w].data_ptr(), h_in[w].data_ptr(), nb, s.cuda_stream) == 0
+                    assert L.dmlc_amd_copy(h_out[w].data_ptr(), d_out[w].data_ptr(), nb // 2, s.cuda_stream) == 0
+                else:
+                    with torch.cuda.stream(s):
+                        d_in[w].copy_(h_in[w], non_blocking=True)
+                        if mode == "dma":
+                            h_out[w].copy_(d_out[w], non_blocking=True)
+                    if mode != "dma":
+                        assert L.dmlc_amd_copy(h_out[w].data_ptr(), d_out[w].data_ptr(), nb // 2, s.cuda_stream) == 0
+            torch.cuda.synchronize()
+            best = min(best, time.perf_counter() - t0)
+        print(json.dumps({"case": "batched_" + mode, "batch_bytes": nb, "GBps_in": round(nb * reps / best / 1e9, 2)}),
               flush=True)
 
 
@@ -75,4 +110,5 @@ def host_memcpy(n=1 << 30, threads=(1, 4, 8, 16)):
 
 if __name__ == "__main__":
     main()
+    batched()
     host_memcpy()

@@ -18,6 +18,8 @@
  *    " # row <r>" (libsvm_parser.h:67-83), and a '#' header line first.
  *  CSV+blank row (fmt 5): the CSV row with ", " between values (ParseFloat
  *    skips the blank before each value, strtonum.h:95-264).
+ *  libsvm 1-based row (fmt 6): the libsvm row with every id one higher (no 0
+ *    id: indexing_mode=-1 shifts them back, libsvm_parser.h:165-171).
  */
 #include <stdint.h>
 #include <stdio.h>
@@ -36,7 +38,7 @@ static inline uint64_t row_state(uint64_t seed, uint64_t r) {
   return s;
 }
 
-static size_t fmt_libsvm_row(char *o, uint64_t seed, uint64_t r, int K, int qid, int cmt) {
+static size_t fmt_libsvm_row(char *o, uint64_t seed, uint64_t r, int K, int qid, int cmt, int one_based) {
   uint64_t s = row_state(seed, r);
   char *p = o;
   *p++ = (char)('0' + (sm64(&s) & 1));
@@ -45,7 +47,7 @@ static size_t fmt_libsvm_row(char *o, uint64_t seed, uint64_t r, int K, int qid,
   for (int j = 0; j < K; ++j) {
     uint64_t x = sm64(&s);
     uint64_t gap = 1 + (x & 15);
-    id = j == 0 ? gap - 1 : id + gap;
+    id = j == 0 ? gap - 1 + (uint64_t)one_based : id + gap;
     float v = (float)(x >> 40) * (1.0f / 16777216.0f);
     p += sprintf(p, " %llu:%.9g", (unsigned long long)id, (double)v);
   }
@@ -84,7 +86,7 @@ static size_t fmt_csv_row(char *o, uint64_t seed, uint64_t r, int C, int blank) 
 
 /* upper bound on the bytes of `nrows` rows */
 size_t synth_bound(int fmt, uint64_t nrows, int width) {
-  return fmt == 0 || fmt == 3 || fmt == 4 ? nrows * (size_t)(2 + 28 + width * 26) + 32
+  return fmt == 0 || fmt == 3 || fmt == 4 || fmt == 6 ? nrows * (size_t)(2 + 28 + width * 26) + 32
                   : fmt == 2 ? nrows * (size_t)(2 + width * 30) : nrows * (size_t)(width * 19 + 2);
 }
 
@@ -107,7 +109,8 @@ size_t synth_rows(int fmt, uint64_t row0, uint64_t nrows, int width, uint64_t se
     for (uint64_t r = r0; r < r1; ++r) {
       if (line_off) line_off[r] = n; /* block-relative; fixed below */
       if (fmt == 4 && row0 + r == 0) n += (size_t)sprintf(buf + n, "# label id:value ... # row r\n");
-      n += fmt == 0 || fmt == 3 || fmt == 4 ? fmt_libsvm_row(buf + n, seed, row0 + r, width, fmt == 3, fmt == 4)
+      n += fmt == 0 || fmt == 3 || fmt == 4 || fmt == 6
+               ? fmt_libsvm_row(buf + n, seed, row0 + r, width, fmt == 3, fmt == 4, fmt == 6)
                     : fmt == 2 ? fmt_libfm_row(buf + n, seed, row0 + r, width)
                                : fmt_csv_row(buf + n, seed, row0 + r, width, fmt == 5);
     }

@@ -7,7 +7,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB = None
 
-LIBSVM, CSV, LIBFM, LIBSVM_QID, LIBSVM_CMT, CSV_SP = 0, 1, 2, 3, 4, 5
+LIBSVM, CSV, LIBFM, LIBSVM_QID, LIBSVM_CMT, CSV_SP, LIBSVM_1B = 0, 1, 2, 3, 4, 5, 6
 
 
 def lib():
