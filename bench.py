@@ -47,6 +47,7 @@ CONFIGS = {
     "libsvm_1b_im1_1m_x128": ("libsvm_1b", 1 << 20, 128, None),  # 1-based ids, ?indexing_mode=-1 (every id shifted)
     "csv_i32_1m_x256": ("csv", 1 << 20, 256, None),        # config 3 parsed as Parser<uint32_t, int32_t>
     "csv_sp_1m_x256": ("csv_sp", 1 << 20, 256, None),      # config 3 with ", " between values
+    "csv_hdr_1m_x256": ("csv", 1 << 20, 256, None),        # config 3 behind a header row of column names
     # the exact kernels (the path input outside the single-pass grammar takes:
     # inf / nan tokens, BOM lines, '#' lines after a range's first line, qid
     # mixes) on configs 2 / 3, forced with DMLC_AMD_FLAG_EXACT
@@ -73,6 +74,7 @@ DESC = {
     "libsvm_1b_im1_1m_x128": "libsvm 1M rows x 128 nnz/row with 1-based ids, indexing_mode=-1 (every range detected 1-based and shifted), device-resident",
     "csv_i32_1m_x256": "CSV dense 1M rows x 256 cols parsed with DType int32 (strtoll), device-resident",
     "csv_sp_1m_x256": "CSV dense 1M rows x 256 float cols, ', ' separators, device-resident",
+    "csv_hdr_1m_x256": "CSV dense 1M rows x 256 float cols behind a header row of column names, device-resident",
     "libsvm_exact_1m_x128": "libsvm 1M rows x 128 nnz/row on the exact kernels (DMLC_AMD_FLAG_EXACT), device-resident",
     "csv_exact_1m_x256": "CSV dense 1M rows x 256 float cols on the exact kernels (DMLC_AMD_FLAG_EXACT), device-resident",
 }
@@ -220,6 +222,9 @@ def main():
         rows = args.rows
     t0 = time.time()
     text, _ = synth.rows(SYNTH[fmt], rows, width, seed=1, row0=rank * rows)
+    if args.config == "csv_hdr_1m_x256":  # a header row: a row without values (csv_fast.h csv_junk_byte)
+        header = np.frombuffer((",".join("feature_%d" % j for j in range(width)) + "\n").encode(), np.uint8)
+        text = np.concatenate([header, text])
     starts = dmlc_amd.text_chunk_starts(text)
     log("[rank %d] generated %s: %d rows, %.3f GB, %d chunks in %.1f s"
         % (rank, args.config, rows, text.size / 1e9, len(starts) - 1, time.time() - t0))

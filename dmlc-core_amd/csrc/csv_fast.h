@@ -61,13 +61,34 @@ struct Shared {  // LDS of one workgroup
                           // LDS footprint -- 16 more bytes cost the plain kernel 8%)
   uint32_t pend[kTile / kPassTokens + 2];  // token counts at the end of each pass
   uint32_t npass;
+  uint32_t junk;  // the tile (or its halos) holds junk bytes (csv_junk_byte)
 };
 
-DA_HD uint32_t class_of_csv(uint32_t b, uint32_t delim, bool blanks) {
+// "Junk" (float values, no label / weight column): text a number ends at
+// (strtonum.h:95-264) -- a header word, a text column, "3.5kg".  A field that
+// starts with it holds no value (ParseFloat consumed nothing: the column
+// advances, csv_parser.h:115-118) -- except where ParseFloat does read it:
+// an 'f' / 'F' is the suffix it consumes (a field "feature_1" is the value 0,
+// which the window decoder yields), and "inf" / "nan" (any case, also after
+// a sign) are values the single pass leaves to the exact kernels
+// (csv_inf_nan).  Not junk: number characters, what ParseFloat skips
+// (isspace) and bytes >= 0x80 (a UTF-8 BOM at a line start).
+DA_HD bool csv_junk_byte(uint32_t b) {
+  return b < 0x80u && b != ' ' && b != '\t' && b != '\v' && b != '\f';
+}
+// the three bytes at p spell "inf" or "nan" (ParseFloat's case-insensitive match)
+DA_HD bool csv_inf_nan(const uint8_t *p) {
+  const uint32_t a = p[0] | 0x20u, b = p[1] | 0x20u, c = p[2] | 0x20u;
+  return (a == 'i' && b == 'n' && c == 'f') || (a == 'n' && b == 'a' && c == 'n');
+}
+// junk: with the junk class (digit + newline, a pair no other byte has; the
+// classifier splits it off)
+DA_HD uint32_t class_of_csv(uint32_t b, uint32_t delim, bool blanks, bool junk = false) {
   if (b == delim) return 0x01000000u;
   if (is_digitchar(b)) return is_digit(b) ? 0x00000101u : 0x00000001u;
   if (b == '\n' || b == '\r') return 0x00010000u;
   if (blanks && (b == ' ' || b == '\t')) return 0u;  // blank: class 0
+  if (junk && csv_junk_byte(b)) return 0x00010100u;
   return 0x00000100u;  // outside the grammar: "digit" without "number char"
 }
 
@@ -202,6 +223,7 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
   // capped the 131k-tile launch at ~1.5 ms.)  Should a predecessor ever not
   // publish, kSpinLimit bounds the wait and the exact kernels take over.
   const int tid = bk.tid();
+  constexpr bool JK = VT == 0 && !SP;  // junk fields in the grammar (csv_junk_byte)
   if (a.skip_if_gated && *a.gate) return;  // fill phase after an exact-path count: block-uniform
   FAST_STAMP(k, 0);
   FAST_STAMP(k, 1);
@@ -217,16 +239,24 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
   if (tid == 0) {
     sh.u.m.d[0] = sh.u.m.n[0] = sh.u.m.l[0] = 0;
     sh.nlab = sh.nfirst = 0;
+    sh.junk = 0;
   }
-  sh.cls[tid] = class_of_csv((uint32_t)tid, a.delim, !SP);
+  sh.cls[tid] = class_of_csv((uint32_t)tid, a.delim, !SP, JK);
   init_dec_tables(sh.dt, bk);
   stage_commit(a.text, a.n, t.tlo, sr, sh.c, bk);
   bk.sync();
   // ---- classify: segment tid -> slot tid+1; lanes 0..15 also one dword
   // each of the 64 bytes before the tile -> slot 0
   uint32_t bad = 0;
+  uint64_t J = 0;  // junk bytes of my segment (JK)
   {
-    const Masks m = classify64_lut(sh.c.text + kPre + tid * kSegB, sh.cls);
+    Masks m = classify64_lut(sh.c.text + kPre + tid * kSegB, sh.cls);
+    if (JK) {  // split the junk class (digit + newline) off the planes
+      J = m.g & m.n;
+      m.g &= ~J;
+      m.n &= ~J;
+      if (J) sh.junk = 1;
+    }
     sh.gw[2 * tid] = (uint32_t)m.g;
     sh.gw[2 * tid + 1] = (uint32_t)(m.g >> 32);
     if (tid == kWave) {  // digits of the 16 bytes after the tile (windows of my last values)
@@ -235,7 +265,9 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
       for (int i = 0; i < 4; ++i) {
         uint32_t x;
         memcpy(&x, sh.c.text + kPre + kTile + 4 * i, 4);
-        g |= classify_dword_lut(x, sh.cls).g << (4 * i);
+        const Nib b = classify_dword_lut(x, sh.cls);
+        g |= (JK ? b.g & ~b.n : b.g) << (4 * i);
+        if (JK && (b.g & b.n)) sh.junk = 1;
       }
       sh.gw[2 * kThreads] = g;
     }
@@ -250,8 +282,10 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
       uint32_t x;
       memcpy(&x, sh.c.text + (kPre - kSegB) + 4 * tid, 4);
       const Nib b = classify_dword_lut(x, sh.cls);
+      const uint32_t jb = JK ? b.g & b.n : 0u;
+      if (jb) sh.junk = 1;
       atomic_or_u64(&sh.u.m.d[0], (uint64_t)b.d << (4 * tid));
-      atomic_or_u64(&sh.u.m.n[0], (uint64_t)b.n << (4 * tid));
+      atomic_or_u64(&sh.u.m.n[0], (uint64_t)(b.n & ~jb) << (4 * tid));
       atomic_or_u64(&sh.u.m.l[0], (uint64_t)b.c << (4 * tid));
     }
   }
@@ -286,10 +320,17 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
       // blanks which follow a delimiter, a newline or a chunk start.
       // A chunk start ends a blank run (the decoder would read past the
       // chunk: bad) and, when blank, starts a run of its own (X).
-      const uint64_t B = ~(D | N | L) & valid, Bs = B & ~S, X = F & B & S;
+      const uint64_t B = ~(D | N | L | J) & valid, Bs = B & ~S, X = F & B & S;
       uint32_t cin = 0;
       if (P > 0 && !(S & 1u)) {
-        const uint64_t nb1 = sh.u.m.d[tid] | n1 | l1;  // non-blank bytes of the segment before
+        uint64_t nb1 = sh.u.m.d[tid] | n1 | l1;  // non-blank bytes of the segment before
+        if (JK && !(nb1 >> 63) && sh.junk) {
+          // its junk bytes are not in the planes: its trailing blanks from its bytes
+          const uint8_t *prev = sh.c.text + kPre + (tid - 1) * kSegB;
+          int j = 63;
+          while (j >= 0 && (prev[j] == ' ' || prev[j] == '\t')) --j;
+          if (j >= 0) nb1 |= 1ull << j;
+        }
         if (!(nb1 >> 63)) {
           if (!nb1) {
             bad = 1;  // 64 blanks in a row: beyond this carry, the exact kernels take it
@@ -305,13 +346,32 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
       uint32_t c1, c2;
       const uint64_t land = (add_carry(Bs, F & Bs, cin, &c1) | add_carry(Bs, X << 1, 0u, &c2)) & ~Bs;
       // the run reaches a newline, a chunk start or the text end: ParseFloat /
-      // strtoll would skip on into the next line (csv_parser.h:99-105)
-      if (land & (N | S | ~valid)) bad = 1;
+      // strtoll would skip on into the next line (csv_parser.h:99-105); or
+      // junk: ParseFloat consumed the blanks, a value (left to the exact kernels)
+      if (land & (N | S | ~valid | J)) bad = 1;
       const uint32_t cout = c1 | c2 | (uint32_t)(X >> 63);
       if (cout && (P + 64 >= a.n || t.is_cs(P + 64))) bad = 1;
       if constexpr (VT == 0) {
         // a blank field ending at a delimiter is ParseFloat's 0 (it consumed the blanks)
         T = (F & D) | (land & (D | L));
+        if (JK && sh.junk) {  // block-uniform
+          // junk field starts: no value, unless ParseFloat reads one there --
+          // the 'f' suffix (the value 0: a token), inf / nan (the exact
+          // kernels; also after a sign: "-inf")
+          const uint8_t *seg = sh.c.text + kPre + tid * kSegB;
+          for (uint64_t m = F & J; m; m &= m - 1) {
+            const uint32_t i = (uint32_t)ctz64(m);
+            if ((seg[i] | 0x20u) == 'f') T |= m & (0 - m);
+            else if (csv_inf_nan(seg + i)) bad = 1;
+          }
+          const uint64_t FD = F & D;
+          uint64_t Jn = J >> 1;  // junk after the byte (a sign's next byte)
+          if (FD >> 63) Jn |= (uint64_t)csv_junk_byte(seg[kSegB]) << 63;
+          for (uint64_t m = FD & Jn; m; m &= m - 1) {
+            const uint32_t i = (uint32_t)ctz64(m), b = seg[i];
+            if ((b == '-' || b == '+') && csv_inf_nan(seg + i + 1)) bad = 1;
+          }
+        }
       } else {
         // strtoll consumed nothing unless a digit follows the optional sign:
         // the field is then a missing value (csv_parser.h:115-118)

@@ -309,7 +309,7 @@ DA_HDF void tile(const LibfmArgs &a, svm::Shared &sh, BK &bk, uint64_t k) {
       bool nxt = sg.hi == a.n;
       if (!nxt) {
         const uint64_t h = sg.hi;
-        nxt = is_nl(h < src.wend ? sh.win[h - abase] : a.text[h]) || is_chunk_start(a.cs, a.nchunk, h);
+        nxt = is_nl(h < src.wend ? (uint32_t)sh.win[h - abase] : gbyte(a.text, h)) || is_chunk_start(a.cs, a.nchunk, h);
       }
       sg.le = (sg.ls >> 1) | ((uint32_t)nxt << (len - 1));
     }

@@ -228,6 +228,46 @@ def uniform_csv(rng, nlines, maxcols=40, delim=",", violate=False):
     return text.encode("latin-1")
 
 
+_JUNK = ["abc", "x1", "?", "#c", '"q"', "col_7", "hello world", "3.5kg", "12abc", "-x", "+", "-", ".", "e",
+         "e5", "1e", "0x1A", "W", "(null)", "$9", "_", "a.b", "1/2", "2021-01-02", "feature", "F", "-f", "name",
+         "index", "id", "int", "NAME", "-nam", "in", "n", "i", "f5", "fin"]
+
+
+def junk_csv(rng, nlines, maxcols=30, delim=",", header=True, violate=False):
+    """CSV with text fields (csv_fast.h csv_junk_byte): a header row of column
+    names, text columns and words among the numbers, numbers followed by text
+    ("3.5kg"): ParseFloat consumes nothing of a field that starts with text
+    (no value, the column advances) and stops at text after a number
+    (csv_parser.h:99-127); an 'f' at a field start is its suffix (the value 0).
+    violate=True adds fields the single pass leaves to the exact kernels:
+    "nan", "inf" (any case, after a sign), text after blanks, a UTF-8 BOM."""
+    ncol = int(rng.integers(1, maxcols + 1))
+    out = []
+    if header:
+        out.append(delim.join("c%d_%s" % (j, "xyz"[j % 3]) for j in range(ncol)))
+    for _ in range(nlines):
+        if rng.random() < 0.03:
+            out.append("")
+            continue
+        fields = []
+        for j in range(ncol if rng.random() < 0.9 else int(rng.integers(1, ncol + 1))):
+            r = rng.random()
+            if r < 0.15:
+                v = _JUNK[int(rng.integers(0, len(_JUNK)))]
+            elif r < 0.2:
+                v = ""
+            else:
+                v = _csv_field(rng)
+            if violate and rng.random() < 0.02:
+                v = rng.choice(["nan", "inf", "Infinity", "NaN(1)", "-inf", "+NAN", "info", " abc", "\xef\xbb\xbf1",
+                                "\t?"])
+            fields.append(v.replace(delim, ";") if delim != ";" else v.replace(delim, ":"))
+        out.append(delim.join(fields))
+    seps = ["\n"] * 12 + ["\r\n", "\r"]
+    text = "".join(line + seps[int(rng.integers(0, len(seps)))] for line in out)
+    return text.encode("latin-1")
+
+
 def dense_csv(rng, nbytes, delim=",", wide=False):
     """CSV of one-digit fields (some empty): up to 8k tokens per 16 KiB tile,
     so the CSV token lists (csv_fast.h kPassTokens) take several passes; rows

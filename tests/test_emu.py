@@ -533,6 +533,34 @@ def test_emu_csv_fast_blanks_and_ints(vt):
     assert paths["fast"] >= 12, paths
 
 
+def test_emu_csv_fast_text_fields():
+    """Text in CSV float columns on the single-pass kernel (csv_fast.h
+    csv_junk_byte): header rows, text columns, words and numbers followed by
+    text -- a field starting with text holds no value, text after a number
+    ends it; "nan"/"inf"/"f" fields, text after blanks and BOMs go to the
+    exact kernels.  Multi-tile, odd chunkings, both ',' and ' ' delimiters."""
+    rng = np.random.default_rng(77)
+    paths = {"fast": 0, "exact": 0}
+    for it in range(40):
+        big = it % 8 == 7
+        violate = it % 5 == 4
+        delim = " " if it % 7 == 3 else ","
+        data = fuzz_text.junk_csv(rng, 1200 if big else int(rng.integers(1, 40)), 40 if big else 12, delim=delim,
+                                  header=it % 2 == 0, violate=violate)
+        offs = fuzz_text.random_cuts(rng, data, 5, anywhere=it % 3 == 1)
+        kw = {"delimiter": delim}
+        o = po.parse_chunks(data, offs, fmt=po.CSV, **kw)
+        h = pyemu.parse(data, offs, "csv", **kw)
+        failed = check_fail(h, "csv", offs)
+        assert (o["status"] != 0) == failed, (it, data[:300], offs, o["msg"], h["error"])
+        if not failed:
+            assert diff(h, o) == [], (it, diff(h, o), data[:300])
+        paths[h["path"]] += 1
+        if not violate and delim == ",":
+            assert h["path"] == "fast", (it, data[:300])
+    assert paths["fast"] >= 20 and paths["exact"] >= 4, paths
+
+
 @pytest.mark.parametrize("vt", [0, 1, 2])
 def test_emu_csv_chunk_cut_edges(vt):
     """Chunk cuts inside blank runs and between a sign and its digits: the

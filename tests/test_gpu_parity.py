@@ -443,6 +443,54 @@ def test_gpu_csv_fast_fuzz_vs_oracle(dm):
     assert paths["fast"] > 150, paths
 
 
+def test_gpu_csv_fast_text_fields_vs_oracle(dm):
+    """Text in CSV float columns on the single-pass kernel (csv_fast.h
+    csv_junk_byte): header rows, text columns, numbers followed by text;
+    "nan"/"inf"/"f" fields, text after blanks and BOMs take the exact kernels.
+    Either path gives the reference's result."""
+    rng = np.random.default_rng(4711)
+    paths = {"fast": 0, "exact": 0}
+    for it in range(160):
+        delim = ",;| "[it % 4]
+        big = it % 16 == 15
+        violate = it % 5 == 4
+        data = fuzz_text.junk_csv(rng, 1500 if big else int(rng.integers(1, 40)), 40 if big else 16, delim,
+                                  header=it % 2 == 0, violate=violate)
+        offs = fuzz_text.random_cuts(rng, data, 6, anywhere=rng.random() < 0.3)
+        try:
+            h = _gpu_vs_oracle_paths(dm, data, offs, fmt=po.CSV, delimiter=delim)
+        except AssertionError as e:
+            raise AssertionError("case %d: %s" % (it, e))
+        paths[h["path"]] += 1
+        if not violate and delim == ",":
+            assert h["path"] == "fast", (it, data[:200])
+    assert paths["fast"] > 80 and paths["exact"] > 10, paths
+
+
+def test_gpu_csv_header_row_bench_shape(dm):
+    """Config 3's shape behind a header row of column names: the single-pass
+    kernel stays on.  Names ParseFloat reads nothing from ("c7") make an empty
+    row; names starting with 'f' ("feature_7") are its suffix, the value 0 in
+    every column (strtonum.h ParseFloat) -- the headerless parse with that row
+    in front."""
+    text, _ = synth.rows(synth.CSV, 60000, 256, seed=5)
+    h0 = gpu_parse(dm, text.tobytes(), dm.text_chunk_starts(text).tolist(), po.CSV)
+    assert not h0["failed"]
+    off0 = np.asarray(h0["offset"]).astype(np.int64)
+    for name, row in (("c%d", 0), ("feature_%d", 256)):
+        header = (",".join(name % j for j in range(256)) + "\n").encode()
+        data = header + text.tobytes()
+        h1 = gpu_parse(dm, data, dm.text_chunk_starts(np.frombuffer(data, np.uint8)).tolist(), po.CSV)
+        assert h1["path"] == "fast" and not h1["failed"], name
+        off1 = np.asarray(h1["offset"]).astype(np.int64)
+        assert off1[:2].tolist() == [0, row], name
+        assert (off1[1:] - row).tolist() == off0.tolist(), name
+        idx1, val1 = np.asarray(h1["index"]), np.asarray(h1["value"])
+        assert idx1[:row].tolist() == list(range(row)) and not np.asarray(val1[:row]).any(), name
+        assert idx1[row:].tobytes() == np.asarray(h0["index"]).tobytes(), name
+        assert val1[row:].tobytes() == np.asarray(h0["value"]).tobytes(), name
+
+
 def test_gpu_csv_fast_multi_tile_vs_oracle(dm):
     """Rows and fields crossing 16 KiB tiles: the segmented column carry
     through the look-back, long rows spanning several tiles."""
