@@ -13,9 +13,10 @@ import torch  # noqa: E402
 import dmlc_amd  # noqa: E402
 from tools import synth  # noqa: E402
 
-fmt, rows, width = {"libsvm": ("libsvm", 1 << 20, 128), "csv": ("csv", 1 << 20, 256)}[
-    sys.argv[1] if len(sys.argv) > 1 else "libsvm"]
-text, _ = synth.rows(synth.LIBSVM if fmt == "libsvm" else synth.CSV, rows, width, seed=1)
+cfg = sys.argv[1] if len(sys.argv) > 1 else "libsvm"
+fmt, rows, width, kind = {"libsvm": ("libsvm", 1 << 20, 128, synth.LIBSVM), "csv": ("csv", 1 << 20, 256, synth.CSV),
+                          "qid": ("libsvm", 1 << 20, 128, synth.LIBSVM_QID)}[cfg]
+text, _ = synth.rows(kind, rows, width, seed=1)
 starts = dmlc_amd.text_chunk_starts(text)
 dev = torch.device("cuda", 0)
 d_text = torch.from_numpy(text).to(dev)
