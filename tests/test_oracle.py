@@ -159,3 +159,22 @@ def test_oracle_filldata_fuzz_vs_reference(fmt):
         if r["status"] == 0:
             assert diff(o, r) == [], (text, kw)
             assert o["blocks"]["rows"].tolist() == r["blocks"]["rows"].tolist()
+
+
+@pytest.mark.skipif(not po.ref_available(), reason="oracle/_ref not built (needs /root/reference)")
+def test_oracle_csv_text_fields_vs_reference():
+    """Live: CSV text fields (header words, text columns, "3.5kg", "feature",
+    "-f", "name", "inf", "NaN(1)", text after blanks) -- what ParseFloat
+    consumes of them (strtonum.h:95-264) -- oracle == the genuine reference."""
+    import fuzz_text
+    rng = np.random.default_rng(4040)
+    for it in range(300):
+        delim = ",;\t|"[it % 4]
+        text = fuzz_text.junk_csv(rng, int(rng.integers(1, 12)), 10, delim=delim, header=it % 3 != 0,
+                                  violate=it % 2 == 1).decode("latin-1")
+        kw = {"fmt": po.CSV, "delimiter": delim}
+        r = po.ref_parse_block(text, **kw)
+        o = po.parse_block(text, **kw)
+        assert (r["status"] != 0) == (o["status"] != 0), (text, r["msg"], o["msg"])
+        if r["status"] == 0:
+            assert diff(o, r) == [], repr(text)
