@@ -119,7 +119,7 @@ hipError_t launch_libfm(const LibfmArgs &a, const FastSvmArgs &f, bool use_fast,
   fm_select_kernel<<<1, 1, 0, s>>>(res, gate, f.err);
   if (phase != kPhaseCount && a.chunk_tab && a.nchunk > 0) chunk_fixup_kernel<<<1, 256, 0, s>>>(a.chunk_tab, a.nchunk, res);
   if (use_fast && phase != kPhaseCount && f.indexing_mode < 0 &&
-      (e = launch_umin_fix(f.index, f.field, f.wide, f.chunk_tab, f.nchunk, f.umin, res, gate, f.cap[C_INDEX], s)) !=
+      (e = launch_umin_fix(f.index, f.field, f.wide, f.chunk_tab, f.nchunk, f.umin, res, gate, f.cap[C_INDEX], f.cap[C_FIELD], s)) !=
           hipSuccess)
     return e;
   return hipGetLastError();

@@ -5,6 +5,8 @@
 //                   the grammar
 //   libsvm_tile     exact count / write tile kernels (libsvm_core.h), run
 //                   only when the gate is set (or indexing_mode < 0)
+#include <atomic>
+
 #include "block.h"
 #include "dmlc_amd_kernels.h"
 #include "libsvm_core.h"
@@ -59,21 +61,27 @@ __global__ void __launch_bounds__(kThreads, FSVM_MINW) svm_fast_tile(FastSvmArgs
 
 // workgroups of a persistent single-pass launch: what the device holds at
 // once (the occupancy calculator, capped at the 6 per CU the LDS budget
-// allows), never more than the tiles
+// allows), never more than the tiles.  The per-device answer is cached in
+// atomics: the engine's workers launch from several host threads.  (The
+// persistent form -- FSVM_PERSIST, off by default -- takes later tiles from a
+// ticket, so it never deadlocks; when other streams' kernels share the device
+// and part of the grid is not resident, the look-back's kSpinLimit valve is
+// what bounds a wait on a tile that is not yet running.)
 template <class K>
 uint32_t persistent_grid(K kernel, uint32_t ntiles) {
-  static int cache_dev[64], cache_n[64];
+  static std::atomic<int> cache_n[64];
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return ntiles;
-  if (cache_n[dev] == 0 || cache_dev[dev] != dev + 1) {
+  int n = cache_n[dev].load(std::memory_order_relaxed);
+  if (n == 0) {
     int cus = 0, per = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, kThreads, 0) != hipSuccess || cus < 1 || per < 1)
       return ntiles;
-    cache_n[dev] = cus * (per < 6 ? per : 6);
-    cache_dev[dev] = dev + 1;
+    n = cus * (per < 6 ? per : 6);
+    cache_n[dev].store(n, std::memory_order_relaxed);
   }
-  return (uint32_t)cache_n[dev] < ntiles ? (uint32_t)cache_n[dev] : ntiles;
+  return (uint32_t)n < ntiles ? (uint32_t)n : ntiles;
 }
 
 // fill phase after a count phase that fell back to the exact kernels: the
@@ -187,7 +195,7 @@ hipError_t launch_libsvm(const LibsvmArgs &a, const FastSvmArgs &f, bool use_fas
   select_kernel<<<1, 1, 0, s>>>(res, gate, f.err);
   if (phase != kPhaseCount && f.chunk_tab && f.nchunk > 0) chunk_fixup_kernel<<<1, 256, 0, s>>>(f.chunk_tab, f.nchunk, res);
   if (use_fast && phase != kPhaseCount && f.indexing_mode < 0 &&
-      (e = launch_umin_fix(f.index, nullptr, f.wide, f.chunk_tab, f.nchunk, f.umin, res, gate, f.cap[C_INDEX], s)) !=
+      (e = launch_umin_fix(f.index, nullptr, f.wide, f.chunk_tab, f.nchunk, f.umin, res, gate, f.cap[C_INDEX], 0, s)) !=
           hipSuccess)
     return e;
   return hipGetLastError();

@@ -1425,20 +1425,28 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
 #if defined(__HIPCC__)
 namespace {  // one private copy per kernel translation unit (no RDC)
 // indexing_mode < 0 after the single-pass write pass (fsvm::umin_fix); every
-// block first checks whether any unit needs the shift, so 0-based input (a 0
-// id in every unit) costs one small read per block.
+// block first checks whether any unit needs the shift -- a unit with ids and
+// no 0 id among them -- so 0-based input costs one small read per block.
+// The shifted range stops at the caller's capacities: res[C_INDEX] is the
+// exact count even when the write pass ran out of room (E_CAPACITY), and the
+// entries past cap_index (cap_field for libfm's field ids) were never stored.
 __global__ void __launch_bounds__(256) umin_fix_kernel(void *index, void *field, int wide, const uint64_t *tab,
                                                        int nunit, const uint64_t *umin, const uint64_t *res,
-                                                       const uint32_t *gate) {
+                                                       const uint32_t *gate, uint64_t cap_index,
+                                                       uint64_t cap_field) {
   if (*gate) return;  // the exact kernels made this result (and applied the rule themselves)
   __shared__ int need;
   if (threadIdx.x == 0) need = 0;
   __syncthreads();
-  for (int u = threadIdx.x; u < nunit; u += 256)
-    if (umin[u] != 0) need = 1;
+  uint64_t total = res[C_INDEX];
+  for (int u = threadIdx.x; u < nunit; u += 256) {
+    const uint64_t uhi = u + 1 < nunit ? tab[(uint64_t)(u + 1) * 8 + C_INDEX] : total;
+    if (umin[u] != 0 && uhi > tab[(uint64_t)u * 8 + C_INDEX]) need = 1;  // ids, none of them 0
+  }
   __syncthreads();
   if (!need) return;
-  const uint64_t total = res[C_INDEX];
+  if (total > cap_index) total = cap_index;
+  if (field && total > cap_field) total = cap_field;
   // a block of 4096 ids inside one unit to shift (the common case: units are
   // InputSplit chunks or their ranges): 16-byte loads, all in flight before
   // the stores; a block across a unit start, 64-bit ids or an unaligned
@@ -1476,11 +1484,12 @@ __global__ void __launch_bounds__(256) umin_fix_kernel(void *index, void *field,
 }
 inline hipError_t launch_umin_fix(void *index, void *field, int wide, const uint64_t *tab, int nunit,
                                   const uint64_t *umin, const uint64_t *res, const uint32_t *gate,
-                                  uint64_t cap_index, hipStream_t s) {
+                                  uint64_t cap_index, uint64_t cap_field, hipStream_t s) {
   if (nunit < 1 || !tab) return hipSuccess;
   uint64_t blocks = (cap_index + 4095) / 4096;
   blocks = blocks < 1 ? 1 : (blocks > 2048 ? 2048 : blocks);
-  umin_fix_kernel<<<(unsigned)blocks, 256, 0, s>>>(index, field, wide, tab, nunit, umin, res, gate);
+  umin_fix_kernel<<<(unsigned)blocks, 256, 0, s>>>(index, field, wide, tab, nunit, umin, res, gate, cap_index,
+                                                   cap_field);
   return hipGetLastError();
 }
 }  // namespace

@@ -128,6 +128,19 @@ dmlc::Parser<I, D> *CreateParser_(const char *uri, unsigned part, unsigned npart
   return (*e->body)(spec.uri, spec.args, part, nparts);
 }
 
+// RowBlockContainer::Push appends `size` weights / qids per block
+// (row_block.h:131-135), so every block stays row-aligned in the container.
+// A libsvm block where only some rows carry label:weight or qid: holds fewer
+// (`own`, this build's parser); the reference reads past them there -- here
+// the block's own values are followed by zeros up to its row count.
+template <typename T>
+void PushPadded(std::vector<T> *dst, const T *src, size_t size, size_t own) {
+  if (src == nullptr) return;
+  if (own > size) own = size;
+  dst->insert(dst->end(), src, src + own);
+  dst->resize(dst->size() + (size - own), T(0));
+}
+
 // BasicRowIter (src/data/basic_row_iter.h:24-79): every block of the parser
 // concatenated as RowBlockContainer::Push does (row_block.h:126-168);
 // NumCol = max_index + 1.  For this build's own parser the block counts and
@@ -173,16 +186,15 @@ class HipRowIter : public dmlc::RowBlockIter<I, D> {
 
  private:
   // RowBlockContainer::Push: labels (zeros for a block without them -- the
-  // reference copies from NULL there), weights / qids of the block's rows,
-  // entries with their maxima, offsets rebased.  With known counts only the
-  // block's own weights / qids are read (the reference reads `size` of them).
+  // reference copies from NULL there), `size` weights / qids per block
+  // (PushPadded), entries with their maxima, offsets rebased.
   void Push(const dmlc::RowBlock<I, D> &b, const BlockCounts *k) {
     const size_t ndata = b.offset[b.size] - b.offset[0];
     const size_t nl = label_.size();
     label_.resize(nl + b.size);
     if (b.label) std::memcpy(label_.data() + nl, b.label, b.size * sizeof(D));
-    if (b.weight) weight_.insert(weight_.end(), b.weight, b.weight + (k ? k->weights : b.size));
-    if (b.qid) qid_.insert(qid_.end(), b.qid, b.qid + (k ? k->qids : b.size));
+    PushPadded(&weight_, b.weight, b.size, k ? k->weights : b.size);
+    PushPadded(&qid_, b.qid, b.size, k ? k->qids : b.size);
     if (b.field) {
       field_.insert(field_.end(), b.field, b.field + ndata);
       if (!k)
@@ -240,15 +252,15 @@ struct Page {
   // row_block.h:126-168; a block without labels (label-less CSV) pushes zeros
   // where the reference copies from its NULL label pointer.  With the block's
   // counts known (this build's parser, k) only its own weights / qids are
-  // read: a libsvm block where some rows lack label:weight or qid: holds fewer
-  // of them than rows, and the reference's `size` of them would read past the
-  // block's share of the pinned batch arrays.
+  // read -- a libsvm block where some rows lack label:weight or qid: holds
+  // fewer of them than rows -- and zeros pad them to the block's rows
+  // (PushPadded), so later blocks stay row-aligned as in the reference.
   void Push(const dmlc::RowBlock<I, D> &b, const BlockCounts *k = nullptr) {
     const size_t n0 = label.size();
     label.resize(n0 + b.size);
     if (b.label) std::memcpy(label.data() + n0, b.label, b.size * sizeof(D));
-    if (b.weight) weight.insert(weight.end(), b.weight, b.weight + (k ? k->weights : b.size));
-    if (b.qid) qid.insert(qid.end(), b.qid, b.qid + (k ? k->qids : b.size));
+    PushPadded(&weight, b.weight, b.size, k ? k->weights : b.size);
+    PushPadded(&qid, b.qid, b.size, k ? k->qids : b.size);
     const size_t ndata = b.offset[b.size] - b.offset[0];
     if (b.field) {
       field.insert(field.end(), b.field, b.field + ndata);

@@ -307,8 +307,9 @@ extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *c
       res[8] = ferr;
       if (imin && !count_only && ftab) {  // chunk_fixup_kernel, then umin_fix_kernel (svm_fast.h)
         chunk_fixup(ftab, nchunks, res);
-        fsvm::umin_fix(a.index, fm ? out->field : nullptr, a.wide, ftab, nchunks, umin.data(), res[C_INDEX], 0,
-                       res[C_INDEX], 0, 1);
+        uint64_t tot = res[C_INDEX] < out->cap[C_INDEX] ? res[C_INDEX] : out->cap[C_INDEX];  // umin_fix_kernel's clamp
+        if (fm && tot > out->cap[C_FIELD]) tot = out->cap[C_FIELD];
+        fsvm::umin_fix(a.index, fm ? out->field : nullptr, a.wide, ftab, nchunks, umin.data(), tot, 0, tot, 0, 1);
       }
     }
     std::fprintf(stderr, "emu: %s path=%s\n", fm ? "libfm" : "libsvm", gate ? "exact" : "fast");

@@ -964,3 +964,48 @@ def test_gpu_fullsize_vs_reference_hashes(dm, name):
         for a in range(0, n, 1 << 26):
             h.update(t[a:min(n, a + (1 << 26))].cpu().numpy().tobytes())
         assert h.hexdigest() == fx["sha256"][k], k
+
+
+@pytest.mark.parametrize("fmt", ["libsvm", "libfm"])
+def test_gpu_umin_fix_stays_inside_capacity(dm, fmt):
+    """indexing_mode=-1 on the single pass with outputs smaller than the
+    counts: the write pass raises the capacity error, and the 1-based shift
+    afterwards (umin_fix_kernel) touches no entry past cap[INDEX] / cap[FIELD]
+    -- guard words after the arrays stay as they were."""
+    import torch
+    rng = np.random.default_rng(11)
+    lines = []
+    for i in range(20000):
+        ids = np.sort(rng.choice(np.arange(1, 5000), 8, replace=False))
+        if fmt == "libsvm":
+            lines.append("%d %s\n" % (i % 2, " ".join("%d:%.3f" % (j, rng.random()) for j in ids)))
+        else:
+            lines.append("%d %s\n" % (i % 2, " ".join("%d:%d:%.3f" % (1 + j % 7, j, rng.random()) for j in ids)))
+    text = "".join(lines).encode()
+    starts = dm.text_chunk_starts(text, 1 << 16)
+    d_text = torch.frombuffer(bytearray(text), dtype=torch.uint8).cuda()
+    d_cs = torch.tensor(starts, device="cuda")
+    p = dm.DeviceParser(fmt, indexing_mode=-1)
+    res = torch.zeros(16, dtype=torch.int64, device="cuda")
+    counts = [int(x) for x in p.count(d_text, d_cs, result=res)]
+    n = counts[dm.INDEX]
+    assert n == 8 * 20000
+    guard = 4096
+    sent = 0x5A5A5A5A
+    out = p.alloc(counts)
+    out["index"] = torch.full((n + guard,), sent, dtype=torch.int32, device="cuda")
+    out["field"] = torch.full((n + guard,), sent, dtype=torch.int32, device="cuda")
+    small = list(counts)
+    small[dm.INDEX] = n // 2
+    if fmt == "libfm":
+        small[dm.FIELD] = n // 3
+    out["counts"] = small
+    p.parse_into(d_text, d_cs, out, res)
+    r = res.cpu().numpy().view(np.uint64)
+    assert dm.error_code(r[8]) == dm.ERR_CAPACITY
+    idx = out["index"].cpu().numpy()
+    assert (idx[small[dm.INDEX]:] == sent).all()
+    assert (idx[:small[dm.INDEX]] != sent).all()
+    if fmt == "libfm":
+        fld = out["field"].cpu().numpy()
+        assert (fld[small[dm.FIELD]:] == sent).all()

@@ -422,8 +422,11 @@ def test_api_copy_modes(tmp_path, mode):
 def test_api_disk_row_cache_partial_weights_and_qids(tmp_path):
     """uri#cachefile over libsvm blocks where only some rows carry label:weight
     or qid: (fewer weights / qids than rows in a block): the cache pages hold
-    exactly the block's own weights and qids (no read past the block's share
-    of the batch arrays) and iterate back equal to the oracle's parse."""
+    each block's own weights and qids followed by zeros up to its row count
+    -- RowBlockContainer::Push appends `size` of them per block
+    (row_block.h:131-135), so later blocks stay row-aligned; the reference
+    reads past the block's values there -- and iterate back equal to the
+    oracle's parse."""
     lines = []
     for i in range(30000):
         lab = b"%d:0.%d" % (i % 2, 1 + i % 9) if i % 3 == 0 else b"%d" % (i % 2)
@@ -441,16 +444,31 @@ def test_api_disk_row_cache_partial_weights_and_qids(tmp_path):
     pages = _cache_pages(cache)
     assert len(pages) == 1
     pg = pages[0]
-    assert pg["weight"].tobytes() == np.asarray(o["weight"], np.float32).tobytes()
-    assert pg["qid"].tolist() == np.asarray(o["qid"]).tolist()
+    blk = o["blocks"]
+    assert len(blk["rows"]) > 1  # several blocks: the padding is per block
+    assert pg["weight"].tobytes() == _pad_per_block(o["weight"], blk["weight"], blk["rows"], np.float32).tobytes()
+    assert pg["qid"].tolist() == _pad_per_block(o["qid"], blk["qid"], blk["rows"], np.uint64).tolist()
     assert pg["offset"].tolist() == np.asarray(o["offset"]).tolist()
     assert pg["index"].tolist() == np.asarray(o["index"]).tolist()
     # iterated back: a RowBlock carries no weight / qid count, so a reader
     # takes `size` of them (as from the reference's own pages); the rest equal
     keep = {k: v for k, v in o.items() if k not in ("weight", "qid")}
     assert diff(h, keep) == []
+    assert h["weight"].tobytes() == pg["weight"].tobytes() and h["qid"].tolist() == pg["qid"].tolist()
     again = run_api(tmp_path, d + "#" + cache, iter_=True)  # the cache reused
-    assert diff(again, keep) == [] and _cache_pages(cache)[0]["weight"].size == 10000
+    assert diff(again, keep) == [] and _cache_pages(cache)[0]["weight"].size == 30000
+
+
+def _pad_per_block(vals, own, rows, dtype):
+    """Each block's own values, then zeros up to its row count (blocks with
+    none contribute nothing: RowBlock.weight / qid is NULL there)."""
+    out, pos = [], 0
+    for k, r in zip(own.tolist(), rows.tolist()):
+        if k:
+            out.append(np.asarray(vals[pos:pos + k], dtype))
+            out.append(np.zeros(r - k, dtype))
+        pos += k
+    return np.concatenate(out) if out else np.zeros(0, dtype)
 
 
 def _cache_pages(path, index_dtype=np.uint32, value_dtype=np.float32):
