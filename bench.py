@@ -43,11 +43,13 @@ CONFIGS = {
     "libsvm_cmt_1m_x128": ("libsvm_cmt", 1 << 20, 128, None),  # config 2's rows with '#' comments
     # grammar variants of configs 2 / 3 (the rates real data hits
     # off the canonical shape)
+    "libsvm_nt2_1m_x128": ("libsvm", 1 << 20, 128, None),  # config 2 at the reference's factory nthread = 2
     "libsvm_im1_1m_x128": ("libsvm", 1 << 20, 128, None),  # config 2 with ?indexing_mode=-1
     "libsvm_1b_im1_1m_x128": ("libsvm_1b", 1 << 20, 128, None),  # 1-based ids, ?indexing_mode=-1 (every id shifted)
     "csv_i32_1m_x256": ("csv", 1 << 20, 256, None),        # config 3 parsed as Parser<uint32_t, int32_t>
     "csv_sp_1m_x256": ("csv_sp", 1 << 20, 256, None),      # config 3 with ", " between values
     "csv_hdr_1m_x256": ("csv", 1 << 20, 256, None),        # config 3 behind a header row of column names
+    "csv_nan_1m_x256": ("csv_nan", 1 << 20, 256, None),    # config 3 with 0.1 % "nan" fields and a BOM at the head
     # the exact kernels (the path input outside the single-pass grammar takes:
     # inf / nan tokens, BOM lines, '#' lines after a range's first line, qid
     # mixes) on configs 2 / 3, forced with DMLC_AMD_FLAG_EXACT
@@ -56,6 +58,7 @@ CONFIGS = {
 }
 # parser arguments per config (dmlc_amd_params; the reference's URI args)
 PARAMS = {
+    "libsvm_nt2_1m_x128": {"nthread": 2},
     "libsvm_im1_1m_x128": {"indexing_mode": -1},
     "libsvm_1b_im1_1m_x128": {"indexing_mode": -1},
     "csv_i32_1m_x256": {"value_type": "i32"},
@@ -70,22 +73,26 @@ DESC = {
     "libfm_1m_x64": "libfm 1M rows x 64 field:id:value/row, device-resident",
     "libsvm_qid_1m_x128": "libsvm 1M rows x 128 nnz/row with qid:<row/16> on every row, device-resident",
     "libsvm_cmt_1m_x128": "libsvm 1M rows x 128 nnz/row, a '# row <r>' comment on every row and a header, device-resident",
+    "libsvm_nt2_1m_x128": "libsvm 1M rows x 128 nnz/row, each InputSplit chunk cut into nthread=2 ParseBlock ranges (the reference's factory default, text_parser.h:32-35), device-resident",
     "libsvm_im1_1m_x128": "libsvm 1M rows x 128 nnz/row, indexing_mode=-1 (per-range 1-based detection), device-resident",
     "libsvm_1b_im1_1m_x128": "libsvm 1M rows x 128 nnz/row with 1-based ids, indexing_mode=-1 (every range detected 1-based and shifted), device-resident",
     "csv_i32_1m_x256": "CSV dense 1M rows x 256 cols parsed with DType int32 (strtoll), device-resident",
     "csv_sp_1m_x256": "CSV dense 1M rows x 256 float cols, ', ' separators, device-resident",
     "csv_hdr_1m_x256": "CSV dense 1M rows x 256 float cols behind a header row of column names, device-resident",
+    "csv_nan_1m_x256": "CSV dense 1M rows x 256 float cols, 0.1% of fields \"nan\", UTF-8 BOM at the file head, device-resident",
     "libsvm_exact_1m_x128": "libsvm 1M rows x 128 nnz/row on the exact kernels (DMLC_AMD_FLAG_EXACT), device-resident",
     "csv_exact_1m_x256": "CSV dense 1M rows x 256 float cols on the exact kernels (DMLC_AMD_FLAG_EXACT), device-resident",
 }
 SYNTH = {"libsvm": synth.LIBSVM, "csv": synth.CSV, "libfm": synth.LIBFM, "libsvm_qid": synth.LIBSVM_QID,
-         "libsvm_cmt": synth.LIBSVM_CMT, "csv_sp": synth.CSV_SP, "libsvm_1b": synth.LIBSVM_1B}
+         "libsvm_cmt": synth.LIBSVM_CMT, "csv_sp": synth.CSV_SP, "libsvm_1b": synth.LIBSVM_1B,
+         "csv_nan": synth.CSV_NAN}
 # the arithmetic the path computes in (values decoded to f32 through the
 # reference's f64 fraction divide; indices / fields as u32)
 DTYPE = {"libsvm": "f32 values / u32 index", "libsvm_1b": "f32 values / u32 index",
          "libsvm_qid": "f32 values / u32 index / u64 qid",
          "libsvm_cmt": "f32 values / u32 index",
-         "csv": "f32 values", "csv_sp": "f32 values", "libfm": "f32 values / u32 index / u32 field"}
+         "csv": "f32 values", "csv_sp": "f32 values", "csv_nan": "f32 values",
+         "libfm": "f32 values / u32 index / u32 field"}
 
 
 def log(*a):
@@ -232,7 +239,8 @@ def main():
     d_text = torch.from_numpy(text).to(dev)
     d_starts = torch.from_numpy(starts).to(dev)
     nbytes = int(text.size)
-    pfmt = {"libsvm_qid": "libsvm", "libsvm_cmt": "libsvm", "libsvm_1b": "libsvm", "csv_sp": "csv"}.get(fmt, fmt)
+    pfmt = {"libsvm_qid": "libsvm", "libsvm_cmt": "libsvm", "libsvm_1b": "libsvm", "csv_sp": "csv",
+            "csv_nan": "csv"}.get(fmt, fmt)
     pkw = dict(PARAMS.get(args.config, {}))
     if pfmt == "csv":
         pkw["label_column"] = args.label_column
@@ -322,8 +330,9 @@ def main():
                    "rows_per_gpu": rows, "width": width, "input_bytes_per_gpu": nbytes,
                    "csr_bytes_per_gpu": b_out, "nnz_per_gpu": int(counts[dmlc_amd.INDEX]),
                    "chunks_per_gpu": len(starts) - 1, "parallelism": par,
+                   "nthread": int(p.params.nthread),  # ParseBlock ranges per chunk (FillData, text_parser.h:116-155)
                    **({"label_column": args.label_column} if args.label_column >= 0 else {}),
-                   **{k: v for k, v in pkw.items() if k != "label_column"}},
+                   **{k: v for k, v in pkw.items() if k not in ("label_column", "nthread")}},
         "hbm_frac_input": round(value / world / HBM_PEAK_GBS, 4),
         "hbm_frac_in_out": round((total_in + b_out * world) * args.steps / elapsed / 1e9
                                  / world / HBM_PEAK_GBS, 4),

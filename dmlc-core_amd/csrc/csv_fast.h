@@ -65,21 +65,46 @@ struct Shared {  // LDS of one workgroup
 };
 
 // "Junk" (float values, no label / weight column): text a number ends at
-// (strtonum.h:95-264) -- a header word, a text column, "3.5kg".  A field that
-// starts with it holds no value (ParseFloat consumed nothing: the column
-// advances, csv_parser.h:115-118) -- except where ParseFloat does read it:
-// an 'f' / 'F' is the suffix it consumes (a field "feature_1" is the value 0,
-// which the window decoder yields), and "inf" / "nan" (any case, also after
-// a sign) are values the single pass leaves to the exact kernels
-// (csv_inf_nan).  Not junk: number characters, what ParseFloat skips
-// (isspace) and bytes >= 0x80 (a UTF-8 BOM at a line start).
-DA_HD bool csv_junk_byte(uint32_t b) {
-  return b < 0x80u && b != ' ' && b != '\t' && b != '\v' && b != '\f';
-}
-// the three bytes at p spell "inf" or "nan" (ParseFloat's case-insensitive match)
-DA_HD bool csv_inf_nan(const uint8_t *p) {
+// (strtonum.h:95-264) -- a header word, a text column, "3.5kg", bytes >=
+// 0x80.  A field that starts with it holds no value (ParseFloat consumed
+// nothing: the column advances, csv_parser.h:115-118) -- except where
+// ParseFloat does read it: an 'f' / 'F' is the suffix it consumes (a field
+// "feature_1" is the value 0, which the window decoder yields), "inf" /
+// "infinity" / "nan" (any case, also after a sign) are the values +-inf and
+// NaN (csv_inf_nan; decoded by inf_nan_of), and junk after blanks is a 0
+// (ParseFloat consumed the blanks).  "nan(" -- ParseFloat's NAN(chars) form
+// with its fatal CHECK for the ')' -- is left to the exact kernels.  A UTF-8
+// BOM at a row start is skipped (IgnoreUTF8BOM, text_parser.h:83-102,
+// csv_parser.h:83): the row's first field starts after it.  Not junk: number
+// characters and what ParseFloat skips (isspace; '\f' and '\v' stay outside
+// the grammar).
+DA_HD bool csv_junk_byte(uint32_t b) { return b != ' ' && b != '\t' && b != '\v' && b != '\f'; }
+// the three bytes at p spell "inf" or "nan" (ParseFloat's case-insensitive
+// match): 1 inf, 2 nan, 3 "nan(", 0 neither
+DA_HD uint32_t csv_inf_nan(const uint8_t *p) {
   const uint32_t a = p[0] | 0x20u, b = p[1] | 0x20u, c = p[2] | 0x20u;
-  return (a == 'i' && b == 'n' && c == 'f') || (a == 'n' && b == 'a' && c == 'n');
+  if (a == 'i' && b == 'n' && c == 'f') return 1u;
+  if (a == 'n' && b == 'a' && c == 'n') return p[3] == '(' ? 3u : 2u;
+  return 0u;
+}
+// ParseFloat's INF / NAN branch (strtonum.h:133-175) on a token window whose
+// first byte after the optional sign is a letter: +-inf ("inf" and
+// "infinity" alike), the quiet NaN (no sign: the reference returns
+// quiet_NaN() whatever the sign), else false (the letters are no number:
+// the window decoder's 0 stands)
+DA_HD bool inf_nan_of(const uint32_t w[4], float *v) {
+  const uint32_t b0 = w[0] & 0xFFu;
+  const uint32_t sg = (b0 == '-' || b0 == '+') ? 1u : 0u;
+  const uint32_t t = funnel(w[1], w[0], 8u * sg) | 0x20202020u;  // the 3 bytes after the sign, lower case
+  if ((t & 0x00FFFFFFu) == 0x00666E69u) {                     // "inf"
+    *v = b0 == '-' ? -__builtin_huge_valf() : __builtin_huge_valf();
+    return true;
+  }
+  if ((t & 0x00FFFFFFu) == 0x006E616Eu) {  // "nan"
+    *v = u2f(0x7FC00000u);
+    return true;
+  }
+  return false;
 }
 // junk: with the junk class (digit + newline, a pair no other byte has; the
 // classifier splits it off)
@@ -308,7 +333,48 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
     const uint64_t n1 = sh.u.m.n[tid], l1 = sh.u.m.l[tid];
     RS = ~N & valid & ((N << 1) | (n1 >> 63) | S);
     const uint64_t FSd = ((L << 1) | (l1 >> 63)) & ~N & ~S & valid;
-    const uint64_t F = RS | FSd;  // field starts
+    uint64_t F = RS | FSd;  // field starts
+    if (JK && sh.junk) {  // block-uniform
+      // a UTF-8 BOM at a row start (IgnoreUTF8BOM, text_parser.h:83-102):
+      // the row's first field starts after it -- in this segment, or in the
+      // next one for a BOM in the last three bytes (that segment sees it
+      // below).  A BOM whose next byte is a newline (the reference's line end
+      // search then starts past it), lies beyond the text, or that holds or
+      // ends at a chunk start goes to the exact kernels.
+      const uint8_t *seg = sh.c.text + kPre + tid * kSegB;
+      auto is_bom = [&](int i) {  // staged bytes seg[i..i+2]
+        return seg[i] == 0xEFu && seg[i + 1] == 0xBBu && seg[i + 2] == 0xBFu;
+      };
+      for (uint64_t m = RS & J; m; m &= m - 1) {
+        const uint32_t i = (uint32_t)ctz64(m);
+        if (!is_bom((int)i)) continue;
+        const uint64_t bit = m & (0 - m);
+        F &= ~bit;
+        if (i <= 60u) {
+          if ((((N | ~valid | S) >> (i + 1u)) & 7u) != 0u) bad = 1;
+          else F |= bit << 3;
+        }
+      }
+      // a BOM that began at a row start in the last three bytes before P
+      for (int i = -3; i < 0; ++i) {
+        const uint64_t x = P + (uint64_t)(int64_t)i;
+        if (P < 3 || !is_bom(i)) continue;
+        // chunk starts before the tile are known only as cfloor (the last one
+        // <= tlo): one inside [x, tlo] leaves the question to the exact kernels
+        if (x < t.tlo && sh.c.cfloor >= x) {
+          bad = 1;
+          continue;
+        }
+        const uint32_t pb = seg[i - 1];
+        const bool cs_x = x == sh.c.cfloor || t.is_cs(x);
+        if (!(cs_x || pb == '\n' || pb == '\r')) continue;  // not a row start: junk
+        const uint32_t j = (uint32_t)(i + 3);  // the field start in this segment (0..2)
+        bool cs_in = (S & ((2ull << j) - 1)) != 0;  // a chunk start inside the BOM or right after it
+        for (uint64_t y = x + 1; y < P; ++y) cs_in = cs_in || y == sh.c.cfloor || t.is_cs(y);
+        if (cs_in || (((N | ~valid) >> j) & 1u)) bad = 1;
+        else F |= 1ull << j;
+      }
+    }
     if constexpr (SP) {
       T = F & D;
     } else {
@@ -346,30 +412,34 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
       uint32_t c1, c2;
       const uint64_t land = (add_carry(Bs, F & Bs, cin, &c1) | add_carry(Bs, X << 1, 0u, &c2)) & ~Bs;
       // the run reaches a newline, a chunk start or the text end: ParseFloat /
-      // strtoll would skip on into the next line (csv_parser.h:99-105); or
-      // junk: ParseFloat consumed the blanks, a value (left to the exact kernels)
-      if (land & (N | S | ~valid | J)) bad = 1;
+      // strtoll would skip on into the next line (csv_parser.h:99-105)
+      if (land & (N | S | ~valid)) bad = 1;
       const uint32_t cout = c1 | c2 | (uint32_t)(X >> 63);
       if (cout && (P + 64 >= a.n || t.is_cs(P + 64))) bad = 1;
       if constexpr (VT == 0) {
-        // a blank field ending at a delimiter is ParseFloat's 0 (it consumed the blanks)
-        T = (F & D) | (land & (D | L));
+        // a blank field ending at a delimiter is ParseFloat's 0 (it consumed
+        // the blanks), and so is one whose blanks run into junk (or into
+        // "inf" / "nan": their value)
+        T = (F & D) | (land & (D | L | J));
         if (JK && sh.junk) {  // block-uniform
           // junk field starts: no value, unless ParseFloat reads one there --
-          // the 'f' suffix (the value 0: a token), inf / nan (the exact
-          // kernels; also after a sign: "-inf")
+          // the 'f' suffix (the value 0: a token), inf / nan (their values,
+          // inf_nan_of; also after a sign: "-inf" is a number-char token);
+          // "nan(" goes to the exact kernels
           const uint8_t *seg = sh.c.text + kPre + tid * kSegB;
           for (uint64_t m = F & J; m; m &= m - 1) {
-            const uint32_t i = (uint32_t)ctz64(m);
-            if ((seg[i] | 0x20u) == 'f') T |= m & (0 - m);
-            else if (csv_inf_nan(seg + i)) bad = 1;
+            const uint32_t i = (uint32_t)ctz64(m), k = csv_inf_nan(seg + i);
+            if (k == 3u) bad = 1;
+            else if (k != 0u || (seg[i] | 0x20u) == 'f') T |= m & (0 - m);
           }
+          for (uint64_t m = land & J; m; m &= m - 1)
+            if (csv_inf_nan(seg + ctz64(m)) == 3u) bad = 1;
           const uint64_t FD = F & D;
           uint64_t Jn = J >> 1;  // junk after the byte (a sign's next byte)
           if (FD >> 63) Jn |= (uint64_t)csv_junk_byte(seg[kSegB]) << 63;
           for (uint64_t m = FD & Jn; m; m &= m - 1) {
             const uint32_t i = (uint32_t)ctz64(m), b = seg[i];
-            if ((b == '-' || b == '+') && csv_inf_nan(seg + i + 1)) bad = 1;
+            if ((b == '-' || b == '+') && csv_inf_nan(seg + i + 1) == 3u) bad = 1;
           }
         }
       } else {
@@ -413,6 +483,7 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
     if (sh.c.bad) atomic_or_u32(a.gate, 1u);
   }
   const bool one_chunk = sh.c.ncs == 0;
+  const bool junk_tile = JK && sh.junk != 0;  // inf / nan tokens possible (block-uniform)
   // the value of the token at q: float (VT 0) or the strtoll result (VT 1)
   using Val = typename std::conditional<VT == 0, float, int64_t>::type;
   auto dec_float = [&](uint64_t q) -> Val {
@@ -424,8 +495,13 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
     if (q + 16 <= lim) {
       const W16 wq = win_at(sh.c.text, t.tlo, q);
       const uint32_t w4[4] = {(uint32_t)wq.lo, (uint32_t)(wq.lo >> 32), (uint32_t)wq.hi, (uint32_t)(wq.hi >> 32)};
-      if constexpr (VT == 0) v = wfloat32m(w4, M, sh.dt, &ok);
-      else v = wint64m(w4, M, &ok);
+      if constexpr (VT == 0) {
+        v = wfloat32m(w4, M, sh.dt, &ok);
+        float x;
+        if (junk_tile && inf_nan_of(w4, &x)) v = x;
+      } else {
+        v = wint64m(w4, M, &ok);
+      }
     }
     if (!ok) {
       GSrc src{a.text, lim};

@@ -238,9 +238,11 @@ def junk_csv(rng, nlines, maxcols=30, delim=",", header=True, violate=False):
     names, text columns and words among the numbers, numbers followed by text
     ("3.5kg"): ParseFloat consumes nothing of a field that starts with text
     (no value, the column advances) and stops at text after a number
-    (csv_parser.h:99-127); an 'f' at a field start is its suffix (the value 0).
-    violate=True adds fields the single pass leaves to the exact kernels:
-    "nan", "inf" (any case, after a sign), text after blanks, a UTF-8 BOM."""
+    (csv_parser.h:99-127); an 'f' at a field start is its suffix (the value 0);
+    "nan" / "inf" / "Infinity" (any case, after a sign or blanks) are values,
+    text after blanks a 0, bytes >= 0x80 junk, and a UTF-8 BOM at a row start
+    is skipped (IgnoreUTF8BOM).  violate=True adds one field the single pass
+    leaves to the exact kernels: ParseFloat's "NaN(...)" form."""
     ncol = int(rng.integers(1, maxcols + 1))
     out = []
     if header:
@@ -258,11 +260,16 @@ def junk_csv(rng, nlines, maxcols=30, delim=",", header=True, violate=False):
                 v = ""
             else:
                 v = _csv_field(rng)
-            if violate and rng.random() < 0.02:
-                v = rng.choice(["nan", "inf", "Infinity", "NaN(1)", "-inf", "+NAN", "info", " abc", "\xef\xbb\xbf1",
-                                "\t?"])
+            if rng.random() < 0.03:
+                v = rng.choice(["nan", "inf", "Infinity", "-inf", "+NAN", "info", " abc", "\xef\xbb\xbf1",
+                                "\t?", " nan", "  -Inf", "nAn", "-nan", "\xe9t\xe9", "in", "na"])
             fields.append(v.replace(delim, ";") if delim != ";" else v.replace(delim, ":"))
-        out.append(delim.join(fields))
+        row = delim.join(fields)
+        bom = "\xef\xbb\xbf" if rng.random() < 0.05 and row[:1] not in ("", "\r") else ""  # (a BOM ending its line: exact)
+        out.append(bom + row)
+    if violate and len(out) > 1:
+        k = int(rng.integers(1, len(out)))
+        out[k] = "NaN(1)" + delim + out[k]
     seps = ["\n"] * 12 + ["\r\n", "\r"]
     text = "".join(line + seps[int(rng.integers(0, len(seps)))] for line in out)
     return text.encode("latin-1")

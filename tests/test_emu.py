@@ -537,8 +537,10 @@ def test_emu_csv_fast_text_fields():
     """Text in CSV float columns on the single-pass kernel (csv_fast.h
     csv_junk_byte): header rows, text columns, words and numbers followed by
     text -- a field starting with text holds no value, text after a number
-    ends it; "nan"/"inf"/"f" fields, text after blanks and BOMs go to the
-    exact kernels.  Multi-tile, odd chunkings, both ',' and ' ' delimiters."""
+    ends it; "nan" / "inf" / "f" fields are values (also after a sign or
+    blanks), text after blanks a 0, a BOM at a row start skipped; "NaN(...)"
+    goes to the exact kernels.  Multi-tile, odd chunkings, both ',' and ' '
+    delimiters."""
     rng = np.random.default_rng(77)
     paths = {"fast": 0, "exact": 0}
     for it in range(40):
@@ -558,6 +560,8 @@ def test_emu_csv_fast_text_fields():
         paths[h["path"]] += 1
         if not violate and delim == ",":
             assert h["path"] == "fast", (it, data[:300])
+        if violate:
+            assert h["path"] == "exact" or failed, (it, data[:300])
     assert paths["fast"] >= 20 and paths["exact"] >= 4, paths
 
 

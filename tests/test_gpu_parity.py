@@ -445,9 +445,10 @@ def test_gpu_csv_fast_fuzz_vs_oracle(dm):
 
 def test_gpu_csv_fast_text_fields_vs_oracle(dm):
     """Text in CSV float columns on the single-pass kernel (csv_fast.h
-    csv_junk_byte): header rows, text columns, numbers followed by text;
-    "nan"/"inf"/"f" fields, text after blanks and BOMs take the exact kernels.
-    Either path gives the reference's result."""
+    csv_junk_byte): header rows, text columns, numbers followed by text,
+    "nan" / "inf" / "f" fields (after signs and blanks too), bytes >= 0x80 and
+    BOMs at row starts stay on it; "NaN(...)" takes the exact kernels.  Either
+    path gives the reference's result."""
     rng = np.random.default_rng(4711)
     paths = {"fast": 0, "exact": 0}
     for it in range(160):
@@ -464,6 +465,8 @@ def test_gpu_csv_fast_text_fields_vs_oracle(dm):
         paths[h["path"]] += 1
         if not violate and delim == ",":
             assert h["path"] == "fast", (it, data[:200])
+        if violate:
+            assert h["path"] == "exact" or h["failed"], (it, data[:200])
     assert paths["fast"] > 80 and paths["exact"] > 10, paths
 
 
@@ -1009,3 +1012,18 @@ def test_gpu_umin_fix_stays_inside_capacity(dm, fmt):
     if fmt == "libfm":
         fld = out["field"].cpu().numpy()
         assert (fld[small[dm.FIELD]:] == sent).all()
+
+
+def test_gpu_csv_nan_bom_bench_shape(dm):
+    """The csv_nan_1m_x256 bench shape -- config 3's rows with 0.1 % of the
+    fields "nan" and a UTF-8 BOM at the file head (tools/synth.c fmt 7) -- on
+    the single-pass kernel, equal to the oracle (NaN bit patterns included)."""
+    text, _ = synth.rows(synth.CSV_NAN, 40000, 256, seed=3)
+    data = text.tobytes()
+    assert data[:3] == b"\xef\xbb\xbf" and data.count(b"nan") > 5000
+    offs = dm.text_chunk_starts(text, 1 << 20).tolist()
+    h = gpu_parse(dm, data, offs, po.CSV)
+    assert h["path"] == "fast" and not h["failed"]
+    o = po.parse_chunks(data, offs, fmt=po.CSV)
+    assert o["status"] == 0 and diff(h, o) == []
+    assert np.isnan(np.asarray(h["value"])).sum() == data.count(b"nan")

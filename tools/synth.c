@@ -20,6 +20,10 @@
  *    skips the blank before each value, strtonum.h:95-264).
  *  libsvm 1-based row (fmt 6): the libsvm row with every id one higher (no 0
  *    id: indexing_mode=-1 shifts them back, libsvm_parser.h:165-171).
+ *  CSV with missing values (fmt 7): the CSV row with 0.1 % of its fields
+ *    "nan" (numpy.savetxt's missing value; ParseFloat's NAN branch,
+ *    strtonum.h:133-175), and a UTF-8 BOM at the head of the file
+ *    (IgnoreUTF8BOM, csv_parser.h:83).
  */
 #include <stdint.h>
 #include <stdio.h>
@@ -72,13 +76,14 @@ static size_t fmt_libfm_row(char *o, uint64_t seed, uint64_t r, int K) {
   return (size_t)(p - o);
 }
 
-static size_t fmt_csv_row(char *o, uint64_t seed, uint64_t r, int C, int blank) {
+static size_t fmt_csv_row(char *o, uint64_t seed, uint64_t r, int C, int blank, int nan) {
   uint64_t s = row_state(seed, r);
   char *p = o;
   for (int j = 0; j < C; ++j) {
     uint64_t x = sm64(&s);
     float v = (float)(x >> 40) * (1.0f / 8388608.0f) - 1.0f;
-    p += sprintf(p, j ? (blank ? ", %.9g" : ",%.9g") : "%.9g", (double)v);
+    if (nan && ((x >> 8) & 0xFFFF) % 1000 == 0) p += sprintf(p, j ? ",nan" : "nan");
+    else p += sprintf(p, j ? (blank ? ", %.9g" : ",%.9g") : "%.9g", (double)v);
   }
   *p++ = '\n';
   return (size_t)(p - o);
@@ -87,7 +92,7 @@ static size_t fmt_csv_row(char *o, uint64_t seed, uint64_t r, int C, int blank) 
 /* upper bound on the bytes of `nrows` rows */
 size_t synth_bound(int fmt, uint64_t nrows, int width) {
   return fmt == 0 || fmt == 3 || fmt == 4 || fmt == 6 ? nrows * (size_t)(2 + 28 + width * 26) + 32
-                  : fmt == 2 ? nrows * (size_t)(2 + width * 30) : nrows * (size_t)(width * 19 + 2);
+                  : fmt == 2 ? nrows * (size_t)(2 + width * 30) : nrows * (size_t)(width * 19 + 2) + 3;
 }
 
 /* Format rows [row0, row0+nrows) into out (capacity cap); returns bytes, or 0
@@ -109,10 +114,11 @@ size_t synth_rows(int fmt, uint64_t row0, uint64_t nrows, int width, uint64_t se
     for (uint64_t r = r0; r < r1; ++r) {
       if (line_off) line_off[r] = n; /* block-relative; fixed below */
       if (fmt == 4 && row0 + r == 0) n += (size_t)sprintf(buf + n, "# label id:value ... # row r\n");
+      if (fmt == 7 && row0 + r == 0) n += (size_t)sprintf(buf + n, "\xEF\xBB\xBF");
       n += fmt == 0 || fmt == 3 || fmt == 4 || fmt == 6
                ? fmt_libsvm_row(buf + n, seed, row0 + r, width, fmt == 3, fmt == 4, fmt == 6)
                     : fmt == 2 ? fmt_libfm_row(buf + n, seed, row0 + r, width)
-                               : fmt_csv_row(buf + n, seed, row0 + r, width, fmt == 5);
+                               : fmt_csv_row(buf + n, seed, row0 + r, width, fmt == 5, fmt == 7);
     }
     bbuf[b] = buf;
     bsz[b] = n;

@@ -7,14 +7,15 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB = None
 
-LIBSVM, CSV, LIBFM, LIBSVM_QID, LIBSVM_CMT, CSV_SP, LIBSVM_1B = 0, 1, 2, 3, 4, 5, 6
+LIBSVM, CSV, LIBFM, LIBSVM_QID, LIBSVM_CMT, CSV_SP, LIBSVM_1B, CSV_NAN = 0, 1, 2, 3, 4, 5, 6, 7
 
 
 def lib():
     global _LIB
     if _LIB is None:
         path = os.path.join(_HERE, "_build", "libsynth.so")
-        if not os.path.exists(path):
+        src = os.path.join(_HERE, "synth.c")
+        if not os.path.exists(path) or os.path.getmtime(path) < os.path.getmtime(src):
             build()
         L = ctypes.CDLL(path)
         L.synth_bound.restype = ctypes.c_size_t
