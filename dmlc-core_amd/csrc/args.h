@@ -82,6 +82,17 @@ struct FastSvmArgs {
 // the persistent launch's ticket word follows them
 constexpr uint64_t kFastLbWords = 5;
 
+// Threads of a single-pass tile (fast_common.h): one wave by default -- a
+// tile's phases then need no barrier between waves and the tiles on a CU
+// hide each other's latencies independently; 256 (four waves, 16 KiB
+// tiles) is the round-3 geometry, kept buildable for A/B timing.
+#ifndef FAST_THREADS
+#define FAST_THREADS 64
+#endif
+constexpr int kFastThreads = FAST_THREADS;
+constexpr uint64_t kFastTileBytes = (uint64_t)kFastThreads * 64;  // 64 text bytes per thread
+constexpr int kFastMaxCs = kFastThreads == 64 ? 16 : 32;           // unit starts per tile (fast_common.h kMaxCs)
+
 // Single-pass uniform-grammar CSV kernel (csv_fast.h).
 constexpr int kLabShards = 64;  // FastCsvArgs::labsum shards, one 64-byte line each
 struct FastCsvArgs {

@@ -1,6 +1,7 @@
 // block.h -- the GPU block policy for the tile bodies: thread id, barrier,
 // block-wide min and exclusive scan over wave64 shuffles + LDS.
 #pragma once
+#include "args.h"
 #include "common.h"
 
 namespace dmlc_amd {
@@ -8,15 +9,24 @@ namespace dmlc_amd {
 // kSlot: bytes per scan slot in the LDS scratch -- the largest scan element
 // the kernel uses (64 for the counter vectors of the exact kernels, 8 for the
 // single-pass kernels, whose LDS budget is tight: fast_common.h kLdsBudget)
-template <int kSlot>
+// NW: waves per workgroup (kWaves for the exact kernels; the single-pass
+// kernels' kFastThreads / kWave, one by default -- then sync() is a wave-level
+// ordering point and the scans stay in registers).
+template <int kSlot, int NW = kWaves>
 struct DevBlockT {
   static_assert(kSlot % 8 == 0 && kSlot >= 8, "8-byte granular slots");
   static constexpr int kSlotU64 = kSlot / 8;
-  // LDS scratch: (kWaves + 1) slots of kSlot bytes
+  // LDS scratch: (NW + 1) slots of kSlot bytes
   uint64_t *scratch;
 
   __device__ __forceinline__ int tid() const { return threadIdx.x; }
-  __device__ __forceinline__ void sync() const { __syncthreads(); }
+  __device__ __forceinline__ void sync() const {
+    if constexpr (NW == 1) {
+      wave_sync();  // one wave: its LDS operations complete in order
+    } else {
+      __syncthreads();
+    }
+  }
   // wave-level: ballot over the 64 lanes, and an LDS-ordering point for a
   // protocol run by one wave (LDS ops of a wave complete in order; the fence
   // stops the compiler from moving LDS accesses across it)
@@ -67,7 +77,7 @@ struct DevBlockT {
     __syncthreads();
     uint64_t r = scratch[0];
 #pragma unroll
-    for (int w = 1; w < kWaves; ++w) r = scratch[w * kSlotU64] < r ? scratch[w * kSlotU64] : r;
+    for (int w = 1; w < NW; ++w) r = scratch[w * kSlotU64] < r ? scratch[w * kSlotU64] : r;
     __syncthreads();
     return r;
   }
@@ -90,11 +100,17 @@ struct DevBlockT {
   __device__ __forceinline__ uint64_t exclusive_add(uint64_t v, uint64_t *total) const {
     const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
     const uint64_t inc = wave_incl_add((uint32_t)v) | ((uint64_t)wave_incl_add((uint32_t)(v >> 32)) << 32);
+    if constexpr (NW == 1) {
+      *total = shfl(inc, kWave - 1);
+      (void)lane;
+      (void)wid;
+      return inc - v;
+    }
     if (lane == kWave - 1) scratch[wid] = inc;
     __syncthreads();
     uint64_t pre = 0, tot = 0;
 #pragma unroll
-    for (int w = 0; w < kWaves; ++w) {
+    for (int w = 0; w < NW; ++w) {
       const uint64_t t = scratch[w];
       pre += w < wid ? t : 0;
       tot += t;
@@ -116,35 +132,43 @@ struct DevBlockT {
       T o = shfl_up(inc, d);
       if (lane >= d) inc = op(o, inc);
     }
+    if constexpr (NW == 1) {  // the wave is the block
+      *total = shfl(inc, kWave - 1);
+      const T up = shfl_up(inc, 1);
+      (void)sc;
+      (void)wid;
+      return lane == 0 ? identity : up;
+    }
     T *slot = reinterpret_cast<T *>(reinterpret_cast<char *>(sc) + kSlot * wid);
     if (lane == kWave - 1) *slot = inc;
     __syncthreads();
     if (threadIdx.x == 0) {
       T acc = *reinterpret_cast<T *>(reinterpret_cast<char *>(sc));
-      for (int w = 1; w < kWaves; ++w) {
+      for (int w = 1; w < NW; ++w) {
         T *sw = reinterpret_cast<T *>(reinterpret_cast<char *>(sc) + kSlot * w);
         T t = *sw;
         *sw = acc;
         acc = op(acc, t);
       }
       *reinterpret_cast<T *>(reinterpret_cast<char *>(sc)) = identity;
-      *reinterpret_cast<T *>(reinterpret_cast<char *>(sc) + kSlot * kWaves) = acc;
+      *reinterpret_cast<T *>(reinterpret_cast<char *>(sc) + kSlot * NW) = acc;
     }
     __syncthreads();
     const T up = shfl_up(inc, 1);
     const T wpre = *reinterpret_cast<T *>(reinterpret_cast<char *>(sc) + kSlot * wid);
     const T ex = lane == 0 ? wpre : op(wpre, up);
-    *total = *reinterpret_cast<T *>(reinterpret_cast<char *>(sc) + kSlot * kWaves);
+    *total = *reinterpret_cast<T *>(reinterpret_cast<char *>(sc) + kSlot * NW);
     __syncthreads();
     return ex;
   }
 };
 
 using DevBlock = DevBlockT<64>;
-using DevBlockS = DevBlockT<8>;  // the single-pass kernels: scan elements <= 8 bytes
+// the single-pass kernels: scan elements <= 8 bytes, kFastThreads per block
+using DevBlockS = DevBlockT<8, kFastThreads / kWave>;
 
 // LDS words the policies need
 constexpr int kBlockScratchU64 = 8 * (kWaves + 1);
-constexpr int kSmallScratchU64 = kWaves + 1;
+constexpr int kSmallScratchU64 = kFastThreads / kWave + 1;
 
 }  // namespace dmlc_amd

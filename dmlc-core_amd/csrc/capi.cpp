@@ -10,7 +10,7 @@
 namespace {
 
 constexpr uint64_t kDefaultTile = 256ull << 10;  // bytes of text owned per workgroup (exact kernels)
-constexpr uint64_t kFastTile = 16ull << 10;      // svm_fast.h kTile
+constexpr uint64_t kFastTile = dmlc_amd::kFastTileBytes;  // fast_common.h kTile
 constexpr int kSlots = 7;
 
 uint64_t tile_of(const dmlc_amd_params *p) {
@@ -105,6 +105,12 @@ int dmlc_amd_profile_end(double *total_ms, int *launches, const char **kernel) {
 
 
 int dmlc_amd_abi_version(void) { return DMLC_AMD_ABI_VERSION; }
+
+int dmlc_amd_fast_geometry(uint32_t *tile_bytes, uint32_t *max_unit_starts) {
+  if (tile_bytes) *tile_bytes = (uint32_t)dmlc_amd::kFastTileBytes;
+  if (max_unit_starts) *max_unit_starts = (uint32_t)dmlc_amd::kFastMaxCs;
+  return DMLC_AMD_OK;
+}
 
 int dmlc_amd_device_count(void) {
   int n = 0;

@@ -24,7 +24,7 @@ static_assert(sizeof(fcsv::Shared) + kSmallScratchU64 * 8 <= fast::kLdsBudget,
 #define FCSV_MINW 6
 #endif
 template <int MODE>
-__global__ void __launch_bounds__(kThreads, FCSV_MINW) csv_fast_tile(FastCsvArgs a) {
+__global__ void __launch_bounds__(fast::kFThreads, FCSV_MINW) csv_fast_tile(FastCsvArgs a) {
   __shared__ __attribute__((aligned(16))) fcsv::Shared sh;
   __shared__ uint64_t scratch[kSmallScratchU64];
   DevBlockS bk{scratch};
@@ -32,7 +32,7 @@ __global__ void __launch_bounds__(kThreads, FCSV_MINW) csv_fast_tile(FastCsvArgs
 }
 // integer DTypes (strtoll)
 template <int MODE>
-__global__ void __launch_bounds__(kThreads, FCSV_MINW) csv_fast_tile_int(FastCsvArgs a) {
+__global__ void __launch_bounds__(fast::kFThreads, FCSV_MINW) csv_fast_tile_int(FastCsvArgs a) {
   __shared__ __attribute__((aligned(16))) fcsv::Shared sh;
   __shared__ uint64_t scratch[kSmallScratchU64];
   DevBlockS bk{scratch};
@@ -40,7 +40,7 @@ __global__ void __launch_bounds__(kThreads, FCSV_MINW) csv_fast_tile_int(FastCsv
 }
 // with a label and / or weight column
 template <int MODE>
-__global__ void __launch_bounds__(kThreads, FCSV_MINW) csv_fast_tile_sp(FastCsvArgs a) {
+__global__ void __launch_bounds__(fast::kFThreads, FCSV_MINW) csv_fast_tile_sp(FastCsvArgs a) {
   __shared__ __attribute__((aligned(16))) fcsv::Shared sh;
   __shared__ uint64_t scratch[kSmallScratchU64];
   DevBlockS bk{scratch};
@@ -103,15 +103,15 @@ hipError_t launch_csv(const CsvArgs &a, const FastCsvArgs &f, bool use_fast, uin
     const bool iv = f.vtype != 0;
     if (phase == kPhaseCount) {
       prof_mark(0, s, iv ? "csv_fast_tile_int<1>" : "csv_fast_tile<1>");
-      if (iv) csv_fast_tile_int<1><<<f.ntiles, kThreads, 0, s>>>(f);
-      else if (sp) csv_fast_tile_sp<1><<<f.ntiles, kThreads, 0, s>>>(f);
-      else csv_fast_tile<1><<<f.ntiles, kThreads, 0, s>>>(f);
+      if (iv) csv_fast_tile_int<1><<<f.ntiles, fast::kFThreads, 0, s>>>(f);
+      else if (sp) csv_fast_tile_sp<1><<<f.ntiles, fast::kFThreads, 0, s>>>(f);
+      else csv_fast_tile<1><<<f.ntiles, fast::kFThreads, 0, s>>>(f);
       prof_mark(1, s, "csv_fast_tile<1>");
     } else {
       prof_mark(0, s, iv ? "csv_fast_tile_int<2>" : "csv_fast_tile<2>");
-      if (iv) csv_fast_tile_int<2><<<f.ntiles, kThreads, 0, s>>>(f);
-      else if (sp) csv_fast_tile_sp<2><<<f.ntiles, kThreads, 0, s>>>(f);
-      else csv_fast_tile<2><<<f.ntiles, kThreads, 0, s>>>(f);
+      if (iv) csv_fast_tile_int<2><<<f.ntiles, fast::kFThreads, 0, s>>>(f);
+      else if (sp) csv_fast_tile_sp<2><<<f.ntiles, fast::kFThreads, 0, s>>>(f);
+      else csv_fast_tile<2><<<f.ntiles, fast::kFThreads, 0, s>>>(f);
       prof_mark(1, s, "csv_fast_tile<2>");
     }
     if (f.label_col >= 0 || f.weight_col >= 0) label_check_kernel<<<1, kLabShards, 0, s>>>(f.labsum, gate);

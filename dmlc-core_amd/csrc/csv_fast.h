@@ -34,9 +34,9 @@ using namespace fast;
 enum { Q_ROWS = 0, Q_VALS = 1, Q_TAIL = 2, Q_FLAG = 3 };
 
 struct Planes {  // slot 0: the segment before the tile; slot t+1: segment t
-  uint64_t d[kThreads + 1];  // number characters
-  uint64_t n[kThreads + 1];  // newlines
-  uint64_t l[kThreads + 1];  // delimiters
+  uint64_t d[kFThreads + 1];  // number characters
+  uint64_t n[kFThreads + 1];  // newlines
+  uint64_t l[kFThreads + 1];  // delimiters
 };
 // token list entries (svm_fast.h's run lists for CSV): tile offset (14 bits),
 // column since the row start or the tile start (17 bits: at most kTile
@@ -52,9 +52,10 @@ struct Shared {  // LDS of one workgroup
     Planes m;
     uint32_t lst[kListCap];
   } u;
-  uint32_t cls[256];  // byte classes: byte 0 number char, 1 digit (without 0: outside the grammar), 2 newline, 3 delimiter
+  uint32_t cls[kClsEntries];  // byte classes: byte 0 number char, 1 digit (without 0: outside the grammar),
+                              // 2 newline, 3 delimiter; bytes >= 0x80 read into dt / gw (fast_common.h)
   DecTables dt;
-  uint32_t gw[2 * kThreads + 2];  // digit plane as words: 2t, 2t+1 segment t; 2 kThreads: the post-halo
+  uint32_t gw[2 * kFThreads + 2];  // digit plane as words: 2t, 2t+1 segment t; 2 kFThreads: the post-halo
   uint64_t segc;      // the tile's segmented carry (delimiters since the last row start before it)
   uint32_t nlab, nfirst;  // label tokens (bits 0-15) and weight tokens (16-31) / first delimiters
                           // of rows in this tile (a tile holds < 2^16 tokens; one word keeps the
@@ -79,12 +80,21 @@ struct Shared {  // LDS of one workgroup
 // characters and what ParseFloat skips (isspace; '\f' and '\v' stay outside
 // the grammar).
 DA_HD bool csv_junk_byte(uint32_t b) { return b != ' ' && b != '\t' && b != '\v' && b != '\f'; }
-// the three bytes at p spell "inf" or "nan" (ParseFloat's case-insensitive
-// match): 1 inf, 2 nan, 3 "nan(", 0 neither
+// Letters of "infinity" matched at p (case-insensitive, at most 8): the
+// reference's INF branch stands only for exactly 3 or 8 of them
+// (strtonum.h:133-148; "infin" is no number)
+DA_HD uint32_t infinity_len(uint64_t lo) {  // lo: the 8 bytes at p, little-endian
+  const uint64_t x = (lo | 0x2020202020202020ull) ^ 0x7974696E69666E69ull;  // "infinity"
+  return x ? (uint32_t)ctz64(x) >> 3 : 8u;
+}
+// the bytes at p start ParseFloat's "inf" / "infinity" or "nan":
+// 1 inf, 2 nan, 3 "nan(" (its NAN(chars) form), 0 neither
 DA_HD uint32_t csv_inf_nan(const uint8_t *p) {
-  const uint32_t a = p[0] | 0x20u, b = p[1] | 0x20u, c = p[2] | 0x20u;
-  if (a == 'i' && b == 'n' && c == 'f') return 1u;
-  if (a == 'n' && b == 'a' && c == 'n') return p[3] == '(' ? 3u : 2u;
+  uint64_t lo = 0;
+  for (int i = 0; i < 8; ++i) lo |= (uint64_t)p[i] << (8 * i);
+  const uint32_t k = infinity_len(lo);
+  if (k == 3u || k == 8u) return 1u;
+  if (((lo | 0x202020u) & 0xFFFFFFu) == 0x6E616Eu) return p[3] == '(' ? 3u : 2u;
   return 0u;
 }
 // ParseFloat's INF / NAN branch (strtonum.h:133-175) on a token window whose
@@ -95,12 +105,14 @@ DA_HD uint32_t csv_inf_nan(const uint8_t *p) {
 DA_HD bool inf_nan_of(const uint32_t w[4], float *v) {
   const uint32_t b0 = w[0] & 0xFFu;
   const uint32_t sg = (b0 == '-' || b0 == '+') ? 1u : 0u;
-  const uint32_t t = funnel(w[1], w[0], 8u * sg) | 0x20202020u;  // the 3 bytes after the sign, lower case
-  if ((t & 0x00FFFFFFu) == 0x00666E69u) {                     // "inf"
+  const uint32_t s8 = 8u * sg;  // the 8 bytes after the sign
+  const uint64_t lo = (uint64_t)funnel(w[1], w[0], s8) | ((uint64_t)funnel(w[2], w[1], s8) << 32);
+  const uint32_t k = infinity_len(lo);
+  if (k == 3u || k == 8u) {
     *v = b0 == '-' ? -__builtin_huge_valf() : __builtin_huge_valf();
     return true;
   }
-  if ((t & 0x00FFFFFFu) == 0x006E616Eu) {  // "nan"
+  if (((uint32_t)lo | 0x202020u) == (((uint32_t)lo & 0xFF000000u) | 0x6E616Eu)) {  // "nan"
     *v = u2f(0x7FC00000u);
     return true;
   }
@@ -258,7 +270,11 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
   t.tlo = (uint64_t)k * kTile;
   t.thi = mn<uint64_t>(t.tlo + kTile, a.n);
   StageRegs sr;
+#if defined(FSVM_GLDS) && defined(__HIP_DEVICE_COMPILE__)
+  stage_issue_lds(a.text, a.n, t.tlo, sr, sh.c, bk);  // text loads first: the chunk search overlaps them
+#else
   stage_issue(a.text, a.n, t.tlo, sr, bk);  // text loads first: the chunk search overlaps them
+#endif
   ChunkProbe cp;  // wave 0: the window load stays in flight through classification
   if (tid < kWave) cp = chunk_list_begin(a.cs, a.nchunk, t.tlo, bk);
   if (tid == 0) {
@@ -266,7 +282,7 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
     sh.nlab = sh.nfirst = 0;
     sh.junk = 0;
   }
-  sh.cls[tid] = class_of_csv((uint32_t)tid, a.delim, !SP, JK);
+  for (int i = tid; i < kClsEntries; i += kFThreads) sh.cls[i] = class_of_csv((uint32_t)i, a.delim, !SP, JK);
   init_dec_tables(sh.dt, bk);
   stage_commit(a.text, a.n, t.tlo, sr, sh.c, bk);
   bk.sync();
@@ -276,6 +292,22 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
   uint64_t J = 0;  // junk bytes of my segment (JK)
   {
     Masks m = classify64_lut(sh.c.text + kPre + tid * kSegB, sh.cls);
+    if (m.hi) {  // bytes >= 0x80 (rare): their classes byte by byte (junk, a delimiter, or outside)
+      const uint8_t *seg = sh.c.text + kPre + tid * kSegB;
+      const uint64_t h = hi_mask64(seg);
+      m.d &= ~h;
+      m.g &= ~h;
+      m.n &= ~h;
+      m.c &= ~h;
+      for (uint64_t mm = h; mm; mm &= mm - 1) {
+        const uint64_t bit = mm & (0 - mm);
+        const uint32_t cb = class_of_csv(seg[ctz64(mm)], a.delim, !SP, JK);
+        if (cb & 1u) m.d |= bit;
+        if ((cb >> 8) & 1u) m.g |= bit;
+        if ((cb >> 16) & 1u) m.n |= bit;
+        if ((cb >> 24) & 1u) m.c |= bit;
+      }
+    }
     if (JK) {  // split the junk class (digit + newline) off the planes
       J = m.g & m.n;
       m.g &= ~J;
@@ -284,17 +316,17 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
     }
     sh.gw[2 * tid] = (uint32_t)m.g;
     sh.gw[2 * tid + 1] = (uint32_t)(m.g >> 32);
-    if (tid == kWave) {  // digits of the 16 bytes after the tile (windows of my last values)
+    if (tid == (kFWaves > 1 ? kWave : kFThreads - 1)) {  // digits of the 16 bytes after the tile (windows of my last values)
       uint32_t g = 0;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         uint32_t x;
         memcpy(&x, sh.c.text + kPre + kTile + 4 * i, 4);
-        const Nib b = classify_dword_lut(x, sh.cls);
+        const Nib b = classify_dword_lut(x, sh.cls);  // (bytes >= 0x80: no digit)
         g |= (JK ? b.g & ~b.n : b.g) << (4 * i);
-        if (JK && (b.g & b.n)) sh.junk = 1;
+        if (JK && ((b.g & b.n) | b.hi)) sh.junk = 1;
       }
-      sh.gw[2 * kThreads] = g;
+      sh.gw[2 * kFThreads] = g;
     }
     sh.u.m.d[tid + 1] = m.d;
     sh.u.m.n[tid + 1] = m.n;
@@ -306,9 +338,10 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
     if (tid < 16 && t.tlo > 0) {
       uint32_t x;
       memcpy(&x, sh.c.text + (kPre - kSegB) + 4 * tid, 4);
-      const Nib b = classify_dword_lut(x, sh.cls);
+      const Nib b = classify_dword_lut(x, sh.cls);  // (bytes >= 0x80: planes clear -- junk for JK)
       const uint32_t jb = JK ? b.g & b.n : 0u;
-      if (jb) sh.junk = 1;
+      if (jb | (JK ? b.hi : 0u)) sh.junk = 1;
+      if (b.hi && a.delim >= 0x80u) bad = 1;  // (a delimiter >= 0x80 in the pre-halo: exact kernels)
       atomic_or_u64(&sh.u.m.d[0], (uint64_t)b.d << (4 * tid));
       atomic_or_u64(&sh.u.m.n[0], (uint64_t)(b.n & ~jb) << (4 * tid));
       atomic_or_u64(&sh.u.m.l[0], (uint64_t)b.c << (4 * tid));
@@ -562,8 +595,8 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
     if (nT > kPassTokens) {  // block-uniform: several passes
       const uint32_t own = (uint32_t)popc64(T);
       mypass = exT / kPassTokens;
-      if (tid == kThreads - 1 || (exT + own) / kPassTokens != mypass) sh.pend[mypass] = exT + own;
-      if (tid == kThreads - 1) sh.npass = mypass + 1;
+      if (tid == kFThreads - 1 || (exT + own) / kPassTokens != mypass) sh.pend[mypass] = exT + own;
+      if (tid == kFThreads - 1) sh.npass = mypass + 1;
       bk.sync();
       np = sh.npass;
       pe0 = sh.pend[0];
@@ -572,7 +605,7 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
     bk.sync();
 #pragma unroll
     for (int u = 0; u < kB; ++u) {
-      const uint32_t j = (uint32_t)tid + (uint32_t)u * kThreads;
+      const uint32_t j = (uint32_t)tid + (uint32_t)u * kFThreads;
       vb[u] = 0;
       if (j < pe0) vb[u] = dec_float(t.tlo + (sh.u.lst[j] & 0x3FFFu));
     }
@@ -699,7 +732,7 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
     };
 #pragma unroll
     for (int u = 0; u < kB; ++u) {
-      const uint32_t j = (uint32_t)tid + (uint32_t)u * kThreads;
+      const uint32_t j = (uint32_t)tid + (uint32_t)u * kFThreads;
       if (j < pe0) put_tok(bVal + j, sh.u.lst[j], vb[u]);
     }
     for (uint32_t p = 0; p < np; ++p) {
@@ -709,7 +742,7 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
         if (mypass == p) build(s0, e0);
         bk.sync();
       }
-      for (uint32_t j = (uint32_t)tid + (p ? 0u : (uint32_t)kB * kThreads); j < e0 - s0; j += kThreads) {
+      for (uint32_t j = (uint32_t)tid + (p ? 0u : (uint32_t)kB * kFThreads); j < e0 - s0; j += kFThreads) {
         const uint32_t e = sh.u.lst[j];
         put_tok(bVal + s0 + j, e, dec_float(t.tlo + (e & 0x3FFFu)));
       }

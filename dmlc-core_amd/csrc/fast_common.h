@@ -10,21 +10,27 @@
 namespace dmlc_amd {
 namespace fast {
 
-// LDS of one single-pass workgroup.  gfx950 allocates LDS in 1280-byte
-// granules (160 KiB / 128): 6 workgroups per CU fit 21 granules each
-// (26,880 bytes), one byte more and the launch drops to 5 per CU (measured:
-// +32 bytes took svm_fast_tile from 1.84 to 2.04 ms).
-constexpr int kLdsGranule = 1280;
-constexpr int kLdsBudget = 21 * kLdsGranule;
+// Tile geometry: kFThreads threads (args.h kFastThreads), 64 text bytes each.
+constexpr int kFThreads = kFastThreads;
+constexpr int kFWaves = kFThreads / kWave;
+static_assert(kFThreads % kWave == 0 && kFWaves >= 1 && kFWaves <= 4, "whole waves, at most four");
 
-constexpr int kSegB = 64;                // bytes per thread (one 64-bit mask)
-constexpr int kTile = kThreads * kSegB;  // 16 KiB of text per tile
-constexpr int kPre = 64;                 // staged bytes before the tile (the segment before it)
+// LDS of one single-pass workgroup.  gfx950 allocates LDS in 1280-byte
+// granules (160 KiB / 128): at four waves per tile, 6 workgroups per CU fit
+// 21 granules each (26,880 bytes), one byte more and the launch dropped to 5
+// per CU (+32 bytes took svm_fast_tile from 1.84 to 2.04 ms); a one-wave
+// tile gets 6 granules (7,680 bytes: 21 workgroups per CU).
+constexpr int kLdsGranule = 1280;
+constexpr int kLdsBudget = (kFWaves == 1 ? 6 : kFWaves == 2 ? 11 : 21) * kLdsGranule;
+
+constexpr int kSegB = 64;                 // bytes per thread (one 64-bit mask)
+constexpr int kTile = kFThreads * kSegB;  // text per tile (4 KiB at one wave)
+constexpr int kPre = 64;                  // staged bytes before the tile (the segment before it)
 // (staging 80 bytes before the tile instead -- 16 more for the qid token
 // checks -- cost 11 % on the 1M x 128 libsvm launch: those read global memory)
-constexpr int kPost = 128;               // staged bytes after it (runs crossing the end)
+constexpr int kPost = kFWaves == 1 ? 64 : 128;  // staged bytes after it (runs crossing the end)
 constexpr int kStage = kPre + kTile + kPost;
-constexpr int kMaxCs = 32;               // chunk starts per tile the fast path accepts
+constexpr int kMaxCs = kFastMaxCs;       // chunk starts per tile the fast path accepts (args.h)
 constexpr uint64_t kAgg = 1ull << 62, kIncl = 2ull << 62, kValMask = (1ull << 62) - 1;
 // look-back rounds without progress before a tile gives up and hands the
 // input to the exact kernels (never expected: a safety valve that bounds the
@@ -66,8 +72,30 @@ constexpr uint32_t kHiA = 0x09220050u, kHiB = 0x00040004u;  // HI[0..7]
 struct Masks {
   uint64_t d, n, c;
   uint32_t bad;
-  uint64_t g;  // table form: byte-1 plane (G digit for libsvm, outside-the-grammar for CSV)
+  uint64_t g;   // table form: byte-1 plane (G digit for libsvm, outside-the-grammar for CSV)
+  uint32_t hi;  // table form: a byte >= 0x80 among the 64 (its planes are not the table's)
 };
+
+// The class tables hold the 128 ASCII bytes (512 bytes of LDS per tile); a
+// byte >= 0x80 still indexes by its value -- on the device the read lands in
+// the tile's next LDS arrays, and its planes are replaced afterwards (Masks.hi,
+// hi_mask64): the index stays one SDWA shift.  Host builds (the emulator) mask
+// the index instead.
+constexpr int kClsEntries = 128;
+DA_HD uint32_t cls_index(uint32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return b & 0xFFu;
+#else
+  return b & 0x7Fu;
+#endif
+}
+// bit i: byte i of the 64 at p (16-byte aligned) is >= 0x80 (rare: a slow loop)
+DA_HD uint64_t hi_mask64(const uint8_t *p) {
+  uint64_t m = 0;
+  for (int i = 0; i < 64; ++i) m |= (uint64_t)(p[i] >> 7) << i;
+  return m;
+}
+DA_HD uint32_t hi_nib4(uint32_t x) { return (((x >> 3) & 0x10101010u) * 0x01020408u) >> 28; }  // bytes >= 0x80
 
 DA_HD uint32_t nib_d(uint32_t cls) {  // digitchar byte flags -> 4 bits
   return ((((cls & 0x07070707u) + 0x7F7F7F7Fu) & 0x80808080u) * 0x00204081u) >> 28;
@@ -97,7 +125,7 @@ DA_HD void load16(const uint8_t *p, uint32_t w[4]) {
 }
 
 struct Nib {
-  uint32_t d, n, c, bad, g;
+  uint32_t d, n, c, bad, g, hi;
 };
 DA_HD Nib classify_dword(uint32_t x) {  // 4-bit masks of 4 bytes; bad: a byte outside the grammar
   const uint32_t cls = classify4(x);
@@ -107,6 +135,7 @@ DA_HD Nib classify_dword(uint32_t x) {  // 4-bit masks of 4 bytes; bad: a byte o
   r.c = nib_c(cls);
   r.bad = ((cls + 0x7F7F7F7Fu) & 0x80808080u) != 0x80808080u || (x & 0x80808080u);
   r.g = 0;
+  r.hi = hi_nib4(x);
   return r;
 }
 
@@ -143,6 +172,8 @@ DA_HD Masks classify64(const uint8_t *p) {
   m.n = nl | ((uint64_t)nh << 32);
   m.c = cl | ((uint64_t)ch << 32);
   m.bad = ((all & 0x80808080u) != 0x80808080u) || (orv & 0x80808080u);
+  m.g = 0;
+  m.hi = (orv & 0x80808080u) != 0u;
   return m;
 }
 
@@ -166,16 +197,18 @@ DA_HD uint32_t class_of(uint32_t b) {
 // Masks of the 64 bytes at p (16-byte aligned) through the class table.
 DA_HD Masks classify64_lut(const uint8_t *p, const uint32_t *cls) {
   uint32_t acc[8];
+  uint32_t orv = 0;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     uint32_t w[4];
     load16(p + 16 * q, w);
+    orv |= w[0] | w[1] | w[2] | w[3];
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int b = 0; b < 4; ++b) {
         const int i = 16 * q + 4 * j + b;
-        const uint32_t x = cls[(w[j] >> (8 * b)) & 0xFFu];
+        const uint32_t x = cls[cls_index((w[j] >> (8 * b)) & 0xFFu)];
         if ((i & 7) == 0) acc[i >> 3] = x;
         else acc[i >> 3] |= x << (i & 7);
       }
@@ -199,20 +232,24 @@ DA_HD Masks classify64_lut(const uint8_t *p, const uint32_t *cls) {
   m.c = pc[0] | ((uint64_t)pc[1] << 32);
   const uint64_t g = pg[0] | ((uint64_t)pg[1] << 32);
   m.g = g;
-  m.bad = (g & ~m.d) != 0;
+  m.hi = (orv & 0x80808080u) != 0u;
+  m.bad = (g & ~m.d) != 0 || m.hi;
   return m;
 }
-// 4 bytes (x) through the table: 4-bit masks
+// 4 bytes (x) through the table: 4-bit masks (a byte >= 0x80: r.hi, planes
+// cleared, bad)
 DA_HD Nib classify_dword_lut(uint32_t x, const uint32_t *cls) {
   uint32_t acc = 0;
 #pragma unroll
-  for (int b = 0; b < 4; ++b) acc |= cls[(x >> (8 * b)) & 0xFFu] << b;
+  for (int b = 0; b < 4; ++b) acc |= cls[cls_index((x >> (8 * b)) & 0xFFu)] << b;
+  const uint32_t h = hi_nib4(x), k = ~h & 0xFu;
   Nib r;
-  r.d = acc & 0xFu;
-  r.n = (acc >> 16) & 0xFu;
-  r.c = (acc >> 24) & 0xFu;
-  r.bad = ((acc >> 8) & ~acc & 0xFu) != 0;
-  r.g = (acc >> 8) & 0xFu;
+  r.d = acc & k;
+  r.n = (acc >> 16) & k;
+  r.c = (acc >> 24) & k;
+  r.g = (acc >> 8) & k;
+  r.bad = (r.g & ~r.d) != 0 || h != 0;
+  r.hi = h;
   return r;
 }
 
@@ -409,8 +446,11 @@ DA_HD uint32_t nd4(uint32_t x) {  // 4 bits: byte i is not '0'..'9' (bytes < 0x8
   return udot4((((x ^ 0x30303030u) + 0x76767676u) >> 7) & 0x01010101u, 0x08040201u, 0u);
 }
 DA_HD uint32_t byte_of(const uint32_t w[4], uint32_t p) {  // window byte p < 16 (one v_perm)
-  const uint32_t hi = (p & 8u) ? w[3] : w[1], lo = (p & 8u) ? w[2] : w[0];
-  return perm_b32(hi, lo, (p & 7u) | 0x0C0C0C00u);
+  // (the four words as values: a select between array elements compiled to
+  // a dynamically indexed private array, i.e. scratch memory)
+  const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3];
+  const bool h = (p & 8u) != 0u;
+  return perm_b32(h ? w3 : w1, h ? w2 : w0, (p & 7u) | 0x0C0C0C00u);
 }
 DA_HD uint64_t low_bytes(uint32_t k) {  // mask of the low k bytes, k <= 8
   return k >= 8 ? ~0ull : ((1ull << (8u * k)) - 1ull);
@@ -437,36 +477,39 @@ DA_HD uint32_t digits_ra(const uint32_t w[4], uint32_t s, uint32_t L) {
 // exponent, long parts or a number that may continue past the window (caller
 // falls back to the byte decoder).
 // M: bit i set when window byte i is not '0'..'9' (16 bits)
+// Straight-line (no early return: a decoder in a loop of the tile kernels
+// must not split the wave's exec mask); the value is meaningless when *ok is
+// false.
 DA_HD float wfloat32m(const uint32_t w[4], uint32_t M, const DecTables &tb, bool *ok) {
   const uint32_t b0 = w[0] & 0xFFu;
   const bool neg = b0 == '-';
   const uint32_t sg = (neg || b0 == '+') ? 1u : 0u;
-  const uint32_t p = (uint32_t)ctz32((M & ~sg) | 0x10000u);
-  *ok = false;
-  if (p >= 16u) return 0.f;
-  const uint32_t c = byte_of(w, p);
+  const uint32_t p = (uint32_t)ctz32((M & ~sg) | 0x10000u);  // 0..16
+  const uint32_t pc = p & 15u;
+  const uint32_t c = byte_of(w, pc);
   const bool dot = c == '.';
-  const uint32_t fs = p + 1u;
-  const uint32_t pe = dot ? (uint32_t)ctz32((M & ~((2u << p) - 1u)) | 0x10000u) : p;
-  if (pe >= 16u) return 0.f;
-  const uint32_t ce = dot ? byte_of(w, pe) : c;
+  const uint32_t fs = pc + 1u;  // 1..16
+  const uint32_t pd = (uint32_t)ctz32((M & ~((2u << pc) - 1u)) | 0x10000u);
+  const uint32_t cd = byte_of(w, pd & 15u);
+  const uint32_t pe = dot ? pd : pc;
+  const uint32_t ce = dot ? cd : c;
   const uint32_t il = p - sg;
-  if ((ce | 0x20u) == 'e' || il > 8u) return 0.f;
-  const uint32_t iv = digits_ra(w, sg, il);
+  *ok = p < 16u && pe < 16u && (ce | 0x20u) != 'e' && il <= 8u;
+  const uint32_t iv = digits_ra(w, sg, il < 8u ? il : 8u);
   // fraction bytes [fs, pe) (empty without a '.', pe < fs): tabulated byte
   // masks of each 8-byte half
-  const uint32_t fs8 = fs < 8u ? fs : 8u, pe8 = pe < 8u ? pe : 8u;
-  const uint32_t fsh = fs > 8u ? fs - 8u : 0u, peh = pe > 8u ? pe - 8u : 0u;
+  const uint32_t pk = pe < 16u ? pe : 16u;
+  const uint32_t fs8 = fs < 8u ? fs : 8u, pe8 = pk < 8u ? pk : 8u;
+  const uint32_t fsh = fs > 8u ? fs - 8u : 0u, peh = pk > 8u ? pk - 8u : 0u;
   const uint64_t flo = ((uint64_t)w[1] << 32 | w[0]) & tb.hib[fs8] & ~tb.hib[pe8];
   const uint64_t fhi = ((uint64_t)w[3] << 32 | w[2]) & tb.hib[fsh] & ~tb.hib[peh];
   const uint32_t fh = dig4((uint32_t)(flo >> 32), dig4((uint32_t)flo, 0u));
   const uint32_t fo = dig4((uint32_t)(fhi >> 32), dig4((uint32_t)fhi, 0u));
   const double v = __builtin_fma((double)fh, 1e8, (double)fo);  // exact: < 10^15
-  const uint32_t e = 16u - fs;                                  // 1..15
+  const uint32_t e = 16u - fs;                                  // 0..15
   const double r = tb.i10[e], t = v * r;
   const double q = __builtin_fma(r, __builtin_fma(-t, tb.p10[e], v), t);
   const float value = (float)iv + (float)q;
-  *ok = true;
   return neg ? -value : value;
 }
 DA_HD float wfloat32(const uint32_t w[4], const DecTables &tb, bool *ok) {
@@ -512,6 +555,15 @@ DA_HD W16 win_at(const uint8_t *text, uint64_t tlo, uint64_t q) {
 
 // the same at tile offset o (position tlo + o)
 DA_HD W16 win_at_o(const uint8_t *text, uint32_t o) {
+#if defined(FSVM_UAWIN) && defined(__HIP_DEVICE_COMPILE__)
+  // one ds_read_b128 at the byte offset (gfx950 LDS takes unaligned reads)
+  uint4 v;
+  __builtin_memcpy(&v, text + o + kPre, 16);
+  W16 q;
+  q.lo = v.x | ((uint64_t)v.y << 32);
+  q.hi = v.z | ((uint64_t)v.w << 32);
+  return q;
+#endif
   const uint32_t off = o + kPre;
   const uint32_t *w = reinterpret_cast<const uint32_t *>(text + (off & ~3u));
   const uint32_t sft = (off & 3u) * 8u;
@@ -616,7 +668,7 @@ DA_HDF void stage(const uint8_t *text, uint64_t n, uint64_t tlo, TileCommon &c, 
   const uint64_t s1 = tlo + kTile + kPost;
   uint8_t *dst = c.text + (s0 + kPre - tlo);
   const uint64_t nunits = (s1 - s0) >> 4;
-  for (uint64_t u = bk.tid(); u < nunits; u += kThreads) {
+  for (uint64_t u = bk.tid(); u < nunits; u += kFThreads) {
     const uint64_t g = s0 + (u << 4);
     uint32_t w[4];
     if (g + 16 <= n) {
@@ -646,12 +698,33 @@ DA_HDF void stage(const uint8_t *text, uint64_t n, uint64_t tlo, TileCommon &c, 
 // of a ~57k-cycle tile.)  Tiles whose staged range leaves the text take the
 // byte-wise path of stage() at commit time.
 constexpr int kStageUnits = kStage / 16;
-constexpr int kStageRounds = (kStageUnits + kThreads - 1) / kThreads;
+constexpr int kStageRounds = (kStageUnits + kFThreads - 1) / kFThreads;
 static_assert(kStage % 16 == 0, "staged range is whole 16-byte units");
 struct StageRegs {
   uint32_t w[kStageRounds][4];
   bool interior;
 };
+#if defined(FSVM_GLDS) && defined(__HIP_DEVICE_COMPILE__)
+// LDS-DMA form (global_load_lds_dwordx4): the staged range is contiguous in
+// HBM and in LDS, so each wave-instruction moves 1 KiB straight into LDS
+// (lane l's 16 bytes at base + 16 l) -- no staging VGPRs, no ds_write; the
+// barrier after stage_commit waits for them (vmcnt).  `c` names the LDS.
+constexpr int kStagePieces = (kStage + kWave * 16 - 1) / (kWave * 16);
+template <class BK>
+DA_HDF void stage_issue_lds(const uint8_t *text, uint64_t n, uint64_t tlo, StageRegs &r, TileCommon &c, BK &bk) {
+  r.interior = tlo >= (uint64_t)kPre && tlo + kTile + kPost <= n;
+  if (!r.interior) return;
+  const uint8_t *src = text + (tlo - kPre);
+  const int t = bk.tid(), lane = t & (kWave - 1), w = t / kWave;
+#pragma unroll
+  for (int q = w; q < kStagePieces; q += kFWaves) {
+    const int off = q * kWave * 16 + lane * 16;
+    if (off < kStage)
+      __builtin_amdgcn_global_load_lds((const void *)(src + off),
+                                       (__attribute__((address_space(3))) void *)(c.text + q * kWave * 16), 16, 0, 0);
+  }
+}
+#endif
 template <class BK>
 DA_HDF void stage_issue(const uint8_t *text, uint64_t n, uint64_t tlo, StageRegs &r, BK &bk) {
   r.interior = tlo >= (uint64_t)kPre && tlo + kTile + kPost <= n;
@@ -660,7 +733,7 @@ DA_HDF void stage_issue(const uint8_t *text, uint64_t n, uint64_t tlo, StageRegs
   const int t = bk.tid();
 #pragma unroll
   for (int i = 0; i < kStageRounds; ++i) {
-    const int u = t + i * kThreads;
+    const int u = t + i * kFThreads;
     if (u < kStageUnits) load16(src + 16 * u, r.w[i]);
   }
 }
@@ -671,10 +744,14 @@ DA_HDF void stage_commit(const uint8_t *text, uint64_t n, uint64_t tlo, const St
     stage(text, n, tlo, c, bk);
     return;
   }
+#if defined(FSVM_GLDS) && defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stage_issue_lds's bytes have landed
+  return;
+#endif
   const int t = bk.tid();
 #pragma unroll
   for (int i = 0; i < kStageRounds; ++i) {
-    const int u = t + i * kThreads;
+    const int u = t + i * kFThreads;
     if (u < kStageUnits) memcpy(c.text + 16 * u, r.w[i], 16);
   }
 }

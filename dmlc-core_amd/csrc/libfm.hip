@@ -25,10 +25,10 @@ static_assert(sizeof(fsvm::Shared) + kSmallScratchU64 * 8 <= fast::kLdsBudget,
               "fm_fast_tile LDS above the 6-workgroup budget (fast_common.h kLdsBudget)");
 
 #ifndef FFM_MINW
-#define FFM_MINW 6
+#define FFM_MINW (fast::kFWaves == 1 ? 5 : 6)
 #endif
 template <int MODE>
-__global__ void __launch_bounds__(kThreads, FFM_MINW) fm_fast_tile(FastSvmArgs a) {
+__global__ void __launch_bounds__(fast::kFThreads, FFM_MINW) fm_fast_tile(FastSvmArgs a) {
   __shared__ __attribute__((aligned(16))) fsvm::Shared sh;
   __shared__ uint64_t scratch[kSmallScratchU64];
   DevBlockS bk{scratch};
@@ -70,13 +70,13 @@ hipError_t launch_libfm(const LibfmArgs &a, const FastSvmArgs &f, bool use_fast,
     if ((e = hipMemsetAsync(f.err, 0xFF, sizeof(uint64_t), s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(f.lb, 0, (size_t)f.ntiles * fast::kLbWords * sizeof(uint64_t), s)) != hipSuccess) return e;
     if (phase == kPhaseCount) {
-      fm_fast_tile<1><<<f.ntiles, kThreads, 0, s>>>(f);
+      fm_fast_tile<1><<<f.ntiles, fast::kFThreads, 0, s>>>(f);
     } else {
       if (f.indexing_mode < 0 &&
           (e = hipMemsetAsync(f.umin, 0xFF, (size_t)f.nchunk * sizeof(uint64_t), s)) != hipSuccess)
         return e;
       prof_mark(0, s, "fm_fast_tile<2>");
-      fm_fast_tile<2><<<f.ntiles, kThreads, 0, s>>>(f);
+      fm_fast_tile<2><<<f.ntiles, fast::kFThreads, 0, s>>>(f);
       prof_mark(1, s, "fm_fast_tile<2>");
     }
   } else if ((e = hipMemsetAsync(f.err, 0xFF, sizeof(uint64_t), s)) != hipSuccess) {

@@ -29,17 +29,17 @@ static_assert(sizeof(fsvm::Shared) + kSmallScratchU64 * 8 <= fast::kLdsBudget,
 
 template <int MODE>
 #ifndef FSVM_MINW
-#define FSVM_MINW 6  // workgroups per CU the fill kernel is register-budgeted for
+#define FSVM_MINW (fast::kFWaves == 1 ? 5 : 6)  // waves per SIMD the fill kernel is register-budgeted for
 #endif
 #ifndef FSVM_PERSIST
 #define FSVM_PERSIST 0  // workgroups loop over tiles (svm_fast.h tile_p)
 #endif
-__global__ void __launch_bounds__(kThreads, FSVM_MINW) svm_fast_tile(FastSvmArgs a) {
+__global__ void __launch_bounds__(fast::kFThreads, FSVM_MINW) svm_fast_tile(FastSvmArgs a) {
   __shared__ __attribute__((aligned(16))) fsvm::Shared sh;
   __shared__ uint64_t scratch[kSmallScratchU64];
 #ifdef FSVM_ABL_PAD_LDS  // occupancy experiment only: pad the workgroup's LDS
   __shared__ uint32_t pad[FSVM_ABL_PAD_LDS / 4];
-  if (a.n == 1) pad[threadIdx.x] = 1, a.res[15] = pad[(threadIdx.x + 1) % kThreads];
+  if (a.n == 1) pad[threadIdx.x] = 1, a.res[15] = pad[(threadIdx.x + 1) % fast::kFThreads];
 #endif
   DevBlockS bk{scratch};
 #if FSVM_PERSIST
@@ -76,9 +76,10 @@ uint32_t persistent_grid(K kernel, uint32_t ntiles) {
   if (n == 0) {
     int cus = 0, per = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, kThreads, 0) != hipSuccess || cus < 1 || per < 1)
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, fast::kFThreads, 0) != hipSuccess || cus < 1 || per < 1)
       return ntiles;
-    n = cus * (per < 6 ? per : 6);
+    const int cap = 6 * kWaves / fast::kFWaves;
+    n = cus * (per < cap ? per : cap);
     cache_n[dev].store(n, std::memory_order_relaxed);
   }
   return (uint32_t)n < ntiles ? (uint32_t)n : ntiles;
@@ -144,14 +145,14 @@ hipError_t launch_libsvm(const LibsvmArgs &a, const FastSvmArgs &f, bool use_fas
     if ((e = hipMemsetAsync(f.qsum, 0, kLabShards * 8 * sizeof(uint64_t), s)) != hipSuccess) return e;
     if (phase == kPhaseCount) {
       prof_mark(0, s, "svm_fast_tile<1>");
-      svm_fast_tile<1><<<FSVM_PERSIST ? persistent_grid(svm_fast_tile<1>, f.ntiles) : f.ntiles, kThreads, 0, s>>>(f);
+      svm_fast_tile<1><<<FSVM_PERSIST ? persistent_grid(svm_fast_tile<1>, f.ntiles) : f.ntiles, fast::kFThreads, 0, s>>>(f);
       prof_mark(1, s, "svm_fast_tile<1>");
     } else {
       if (f.indexing_mode < 0 &&
           (e = hipMemsetAsync(f.umin, 0xFF, (size_t)f.nchunk * sizeof(uint64_t), s)) != hipSuccess)
         return e;
       prof_mark(0, s, "svm_fast_tile<2>");
-      svm_fast_tile<2><<<FSVM_PERSIST ? persistent_grid(svm_fast_tile<2>, f.ntiles) : f.ntiles, kThreads, 0, s>>>(f);
+      svm_fast_tile<2><<<FSVM_PERSIST ? persistent_grid(svm_fast_tile<2>, f.ntiles) : f.ntiles, fast::kFThreads, 0, s>>>(f);
       prof_mark(1, s, "svm_fast_tile<2>");
     }
     qid_fix_kernel<<<1, 256, 0, s>>>(f.qsum, res, gate, phase != kPhaseCount ? f.chunk_tab : nullptr, f.nchunk);

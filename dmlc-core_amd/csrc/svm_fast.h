@@ -125,10 +125,12 @@ DA_HD bool qid_clean(uint64_t P, uint64_t *n, uint64_t *c, bool lead, At at, Wd 
 enum { Q_ROWS = 0, Q_INDEX = 1, Q_VALUE = 2, Q_WEIGHT = 3 };
 
 struct Planes {  // slot 0: the segment before the tile; slot t+1: segment t
-  uint64_t d[kThreads + 1];  // digitchar
-  uint64_t n[kThreads + 1];  // newline
-  uint64_t c[kThreads + 1];  // ':'
+  uint64_t d[kFThreads + 1];  // digitchar
+  uint64_t n[kFThreads + 1];  // newline
+  uint64_t c[kFThreads + 1];  // ':'
 };
+// the lane that classifies the 16 bytes after the tile (besides its segment)
+constexpr int kPostLane = kFWaves > 1 ? kWave : kFThreads - 1;
 // run list entries (tile offsets) that fit in the planes' space, which the
 // libsvm write pass no longer reads once the roles are known
 constexpr int kListCap = (int)(sizeof(Planes) / sizeof(uint16_t));
@@ -138,13 +140,13 @@ constexpr uint32_t kPassRuns = (uint32_t)kListCap - kSegB;
 
 struct Shared {  // LDS of one workgroup
   TileCommon c;
-  uint32_t cls[256];  // byte class table (fast_common.h class_of)
+  uint32_t cls[kClsEntries];  // byte class table (fast_common.h class_of); bytes >= 0x80 read into dt / u
   DecTables dt;
   union {
     Planes m;
     uint16_t lst[kListCap];
   } u;
-  uint32_t gw[2 * kThreads + 2];  // digit plane as words: 2t, 2t+1 segment t; 2 kThreads: the post-halo
+  uint32_t gw[2 * kFThreads + 2];  // digit plane as words: 2t, 2t+1 segment t; 2 kFThreads: the post-halo
   uint64_t pend[kTile / kPassRuns + 2];  // packed inclusive counts at the end of each pass
   uint32_t npass;
   uint32_t next;   // persistent form: the next tile id
@@ -160,7 +162,7 @@ struct Tile {
   // masks of the absolute 64-byte segment g (full segments only when g < tlo/64)
   DA_HD void seg(uint64_t g, uint64_t *d, uint64_t *n, uint64_t *c) const {
     const uint64_t g0 = tlo >> 6;
-    if (g < g0 + kThreads && (g >= g0 || (tlo > 0 && g + 1 == g0))) {
+    if (g < g0 + kFThreads && (g >= g0 || (tlo > 0 && g + 1 == g0))) {
       const uint64_t s = g + 1 - g0;
       *d = sh->u.m.d[s];
       *n = sh->u.m.n[s];
@@ -468,7 +470,7 @@ DA_HDF uint32_t comment_erase(uint64_t tlo, uint64_t thi, uint64_t n, TileCommon
   // wave 0: the pre-halo's masks; wave 3: the post-halo's
   CmtMasks kh{0, 0, 0, 0}, kp[kPost / kSegB];
   if (tid < kWave && tlo > 0) kh = wave_cmt_masks(txt, bk);
-  if (tid >= kThreads - kWave)
+  if (tid >= kFThreads - kWave)
     for (int s = 0; s < kPost / kSegB; ++s) kp[s] = wave_cmt_masks(txt + kPre + kTile + s * kSegB, bk);
   const uint64_t S = cs_bits(c, P);
   // the pre-halo read on its own (reach-in 0, no comment open before it): the
@@ -489,7 +491,7 @@ DA_HDF uint32_t comment_erase(uint64_t tlo, uint64_t thi, uint64_t n, TileCommon
   comment_ab(k, S, r, &A, &B);
   const uint32_t f = comment_fn(A, B);
   uint32_t f_next = 0;  // the next tile's reading of its pre-halo (this segment)
-  if (tid == kThreads - 1) {
+  if (tid == kFThreads - 1) {
     uint64_t An, Bn;
     comment_ab(k, S, 0u, &An, &Bn);
     f_next = comment_fn(An, Bn) & 1u;
@@ -509,9 +511,9 @@ DA_HDF uint32_t comment_erase(uint64_t tlo, uint64_t thi, uint64_t n, TileCommon
     wave_blank(txt, Mh, 0u, bk);
     if (tid == 0 && Mh) changed |= 2u;
   }
-  if (tid >= kThreads - kWave) {  // wave 3: lane 63's post-halo comment bytes
-    uint64_t Mp[kPost / kSegB] = {0, 0};
-    if (tid == kThreads - 1) {
+  if (tid >= kFThreads - kWave) {  // the last wave: lane 63's post-halo comment bytes
+    uint64_t Mp[kPost / kSegB] = {};
+    if (tid == kFThreads - 1) {
       if (thi < n && P + kSegB == thi && !(cs_bits(c, thi) & 1u) && co != f_next) gate = 1;
       uint32_t ci = co, ri;
       (void)reach_of(k, S, r, &ri);
@@ -869,7 +871,7 @@ template <bool FM, class At>
 DA_HDF uint32_t classify_tile(const Tile &t, Shared &sh, int tid, At at, bool first, uint32_t parts) {
   uint32_t bad = 0;
   if (parts & 1u) bad = commit_seg<FM>(t, sh, tid, at, first, classify64_lut(sh.c.text + kPre + tid * kSegB, sh.cls));
-  if ((parts & 4u) && tid == kWave) {  // digits of the 16 bytes after the tile (windows of my last runs)
+  if ((parts & 4u) && tid == kPostLane) {  // digits of the 16 bytes after the tile (windows of my last runs)
     uint32_t g = 0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -877,7 +879,7 @@ DA_HDF uint32_t classify_tile(const Tile &t, Shared &sh, int tid, At at, bool fi
       memcpy(&x, sh.c.text + kPre + kTile + 4 * i, 4);
       g |= classify_dword_lut(x, sh.cls).g << (4 * i);
     }
-    sh.gw[2 * kThreads] = g;
+    sh.gw[2 * kFThreads] = g;
   }
   if ((parts & 2u) && tid < 16 && t.tlo > 0) {
     uint32_t x;
@@ -920,7 +922,8 @@ DA_HDF uint32_t comments_reclassify(const Tile t, Shared &sh, uint32_t bad0, BK 
   uint32_t bad = bad0;
   for (uint64_t m = bk.ballot((e >> 1) & 1u); m; m &= m - 1) {  // wave-uniform
     const uint32_t sg = wbase + (uint32_t)ctz64(m);
-    const uint32_t x = sh.cls[sh.c.text[kPre + sg * kSegB + lane]];
+    const uint32_t b = sh.c.text[kPre + sg * kSegB + lane];
+    const uint32_t x = b >= 0x80u ? 0x00000100u : sh.cls[b];  // (>= 0x80: outside the grammar)
     Masks mm;
     mm.d = bk.ballot(x & 1u);
     mm.g = bk.ballot((x >> 8) & 1u);
@@ -940,7 +943,7 @@ DA_HDF uint32_t comments_reclassify(const Tile t, Shared &sh, uint32_t bad0, BK 
 // or once per workgroup in the persistent form.
 template <class BK>
 DA_HDF void init_tables(Shared &sh, BK &bk) {
-  sh.cls[bk.tid()] = class_of((uint32_t)bk.tid());
+  for (int i = bk.tid(); i < kClsEntries; i += kFThreads) sh.cls[i] = class_of((uint32_t)i);
   init_dec_tables(sh.dt, bk);
 }
 
@@ -974,7 +977,11 @@ DA_HDF uint32_t tile_p(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k, Sta
   t.thi = mn<uint64_t>(t.tlo + kTile, a.n);
   uint32_t knext = a.ntiles;  // thread 0: the ticket's answer (PERSIST)
   if (PERSIST && tid == 0) knext = gridDim_x() + atomic_add_u32(a.ticket, 1u);
+#if defined(FSVM_GLDS) && defined(__HIP_DEVICE_COMPILE__)
+  if (!PERSIST) stage_issue_lds(a.text, a.n, t.tlo, sr, sh.c, bk);  // text loads first: the chunk search overlaps them
+#else
   if (!PERSIST) stage_issue(a.text, a.n, t.tlo, sr, bk);  // text loads first: the chunk search overlaps them
+#endif
   ChunkProbe cp;  // wave 0: the window load stays in flight through classification
   if (tid < kWave) cp = chunk_list_begin(a.cs, a.nchunk, t.tlo, bk);
   FAST_STAMP(k, 11);
@@ -1066,6 +1073,11 @@ DA_HDF uint32_t tile_p(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k, Sta
   auto lim_of = [&](uint64_t q) { return one_chunk ? sh.c.cnext : t.next_cs(q); };
   // non-digit flags of the 16 window bytes at tile offset o (bits 16+ unused)
   auto ndig_at = [&](uint32_t o) -> uint32_t {
+#if defined(FSVM_UAWIN) && defined(__HIP_DEVICE_COMPILE__)
+    uint32_t x;  // the plane bytes from o / 8 on: one unaligned ds_read_b32
+    __builtin_memcpy(&x, reinterpret_cast<const uint8_t *>(sh.gw) + (o >> 3), 4);
+    return ~(x >> (o & 7u));
+#endif
     const uint32_t i = o >> 5;
     return ~funnel(sh.gw[i + 1], sh.gw[i], o & 31u);
   };
@@ -1084,7 +1096,9 @@ DA_HDF uint32_t tile_p(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k, Sta
     *ok = k1 && o + 16u <= limr_of(o);
     return v;
   };
-  auto win_index = [&](uint32_t o, bool *ok) -> uint64_t {
+  // the id as read (<= 8 digits: 32 bits); ids_of applies indexing_mode > 0
+  // in the index width
+  auto win_index = [&](uint32_t o, bool *ok) -> uint32_t {
 #ifdef FSVM_ABL_NODEC
     *ok = true;
     return o;
@@ -1095,8 +1109,9 @@ DA_HDF uint32_t tile_p(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k, Sta
     bool k1;
     const bool pos = wuint32m(w4, ndig_at(o), sh.dt, &v, &k1);
     *ok = k1 && pos && o + 16u <= limr_of(o);
-    return a.indexing_mode > 0 ? v - 1 : v;
+    return (uint32_t)v;
   };
+  auto ids_of = [&](uint32_t v) -> uint64_t { return (uint64_t)v - (a.indexing_mode > 0 ? 1u : 0u); };
   auto slow_flt = [&](uint32_t o) -> float { return slow_float(a.text, t.tlo + o, lim_of(t.tlo + o)); };
   auto slow_idx = [&](uint32_t o) -> uint64_t {
     uint64_t v = 0;
@@ -1106,23 +1121,20 @@ DA_HDF uint32_t tile_p(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k, Sta
     }
     return a.indexing_mode > 0 ? v - 1 : v;
   };
-  auto dec_float = [&](uint32_t o) -> float {
-    bool ok;
-    const float v = win_float(o, &ok);
-    return ok ? v : slow_flt(o);
-  };
-  auto dec_index = [&](uint32_t o) -> uint64_t {
-    bool ok;
-    const uint64_t v = win_index(o, &ok);
-    return ok ? v : slow_idx(o);
-  };
+  // A run the window decoders leave (ok false: an exponent, a long number,
+  // a window past its chunk, a '-' index) is not decoded in place: its
+  // entry's bit goes to a per-thread mask (bit u: list entry tid + 256 u of
+  // the pass) and one loop per pass runs the byte decoders on those entries
+  // -- one inlined copy of them, off the hot loops' straight-line code.
 #ifndef FSVM_KB
 #define FSVM_KB 3
 #endif
   constexpr int kB = FSVM_KB;  // runs per decoder decoded before the look-back
   static_assert(kB >= 1 && kB <= 5, "batch positions are packed 6 bits each");
-  uint64_t ib[kB];
+  static_assert((kListCap + kFThreads - 1) / kFThreads <= 32, "slow-entry masks hold one bit per list round");
+  uint32_t ib[kB];
   float fb[kB];
+  uint32_t slowI = 0, slowF = 0;  // this pass's list rounds whose run takes the byte decoders
   // packed counts (fields as `mine`)
   auto fL = [](uint64_t x) { return (uint32_t)(x & 0xFFFF); };
   auto fW = [](uint64_t x) { return (uint32_t)((x >> 16) & 0xFFFF); };
@@ -1171,8 +1183,8 @@ DA_HDF uint32_t tile_p(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k, Sta
       const uint32_t own = fL(mine) + fW(mine) + kIW * fI(mine) + fV(mine);
       const uint32_t tex = fL(ex) + fW(ex) + kIW * fI(ex) + fV(ex);
       mypass = tex / kPassRuns;
-      if (tid == kThreads - 1 || (tex + own) / kPassRuns != mypass) sh.pend[mypass] = ex + mine;
-      if (tid == kThreads - 1) sh.npass = mypass + 1;
+      if (tid == kFThreads - 1 || (tex + own) / kPassRuns != mypass) sh.pend[mypass] = ex + mine;
+      if (tid == kFThreads - 1) sh.npass = mypass + 1;
       bk.sync();
       np = sh.npass;
       pe0 = sh.pend[0];
@@ -1184,11 +1196,14 @@ DA_HDF uint32_t tile_p(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k, Sta
     const uint32_t nI0 = fI(pe0), nF0 = fV(pe0) + fL(pe0) + fW(pe0), fb0 = kIW * nI0;
 #pragma unroll
     for (int u = 0; u < kB; ++u) {
-      const uint32_t j = (uint32_t)tid + (uint32_t)u * kThreads;
+      const uint32_t j = (uint32_t)tid + (uint32_t)u * kFThreads;
       ib[u] = 0;
       fb[u] = 0.f;
-      if (j < nI0) ib[u] = dec_index(sh.u.lst[j]);
-      if (j < nF0) fb[u] = dec_float(sh.u.lst[fb0 + j]);
+      bool oki = true, okf = true;
+      if (j < nI0) ib[u] = win_index(sh.u.lst[j], &oki);
+      if (j < nF0) fb[u] = win_float(sh.u.lst[fb0 + j], &okf);
+      slowI |= (oki ? 0u : 1u) << u;
+      slowF |= (okf ? 0u : 1u) << u;
     }
     FAST_STAMP(k, 6);
   }
@@ -1320,41 +1335,8 @@ DA_HDF uint32_t tile_p(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k, Sta
       raise_error(a.err, E_CAPACITY, q);
     }
   };
-  constexpr uint32_t kIW = FM ? 2u : 1u;  // list entries per index
-  {  // the register batch (pass 0)
-    const uint32_t nI0 = fI(pe0), nV0 = fV(pe0), nL0 = fL(pe0), nF0 = nV0 + nL0 + fW(pe0), fb0 = kIW * nI0;
-#pragma unroll
-    for (int u = 0; u < kB; ++u) {
-      const uint32_t j = (uint32_t)tid + (uint32_t)u * kThreads;
-      if (j < nI0) put_index(bIdx + j, ib[u], t.tlo + sh.u.lst[j]);
-      if (j < nF0) put_float(j, fb[u], sh.u.lst[fb0 + j], 0, nV0, nL0);
-    }
-  }
-#ifndef FSVM_PF_LATE
-  // the next tile's text loads, in flight through the rest of this tile
-  if (PERSIST && kn < a.ntiles) stage_issue(a.text, a.n, (uint64_t)kn * kTile, sr, bk);
-#endif
-  for (uint32_t p = 0; p < np; ++p) {
-    const uint64_t s = p ? sh.pend[p - 1] : 0, e = p ? sh.pend[p] : pe0;
-    if (p) {  // block-uniform
-      bk.sync();
-      if (mypass == p) build(s, e);
-      bk.sync();
-    }
-    const uint64_t cn = e - s;
-    const uint32_t nIp = fI(cn), nVp = fV(cn), nLp = fL(cn), nFp = nVp + nLp + fW(cn), fbp = kIW * nIp;
-    const uint32_t j0 = (uint32_t)tid + (p ? 0u : (uint32_t)kB * kThreads);
-    for (uint32_t j = j0; j < nIp; j += kThreads) {
-      const uint32_t o = sh.u.lst[j];
-      put_index(bIdx + fI(s) + j, dec_index(o), t.tlo + o);
-    }
-    for (uint32_t j = j0; j < nFp; j += kThreads) {
-      const uint32_t o = sh.u.lst[fbp + j];
-      put_float(j, dec_float(o), o, s, nVp, nLp);
-    }
-    if constexpr (FM)
-      for (uint32_t j = (uint32_t)tid; j < nIp; j += kThreads) put_field(bIdx + fI(s) + j, sh.u.lst[nIp + j]);
-  }
+  // Row offsets, qids and the chunk table first: the segment's role masks
+  // die here instead of staying live through the decode loops below.
   // each row's offset: the indices before its label
   uint64_t rl = eL;
   for (uint64_t m = so.L; m; m &= m - 1, ++rl) {
@@ -1386,11 +1368,6 @@ DA_HDF uint32_t tile_p(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k, Sta
       if (sh.c.text[q - t.tlo + kPre] == '-') raise_error(a.err, E_NEG_INDEX, q);
     }
   }
-  if (imin && one_chunk) {  // block-uniform: one store per wave that saw a 0 id
-    const uint64_t zm = bk.ballot(zero);
-    if ((tid & (kWave - 1)) == 0 && zm) store_flag_u64(&a.umin[sh.c.c_first - 1], 0);
-  }
-  FAST_STAMP(k, 8);
   // ---- per-chunk exclusive counts at each chunk start in my segment
   if (a.chunk_tab) {
     for (uint32_t i = 0; i < sh.c.ncs; ++i) {
@@ -1408,6 +1385,62 @@ DA_HDF uint32_t tile_p(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k, Sta
       row[C_FIELD] = FM ? row[C_INDEX] : 0;
     }
   }
+  constexpr uint32_t kIW = FM ? 2u : 1u;  // list entries per index
+  {  // the register batch (pass 0)
+    const uint32_t nI0 = fI(pe0), nV0 = fV(pe0), nL0 = fL(pe0), nF0 = nV0 + nL0 + fW(pe0), fb0 = kIW * nI0;
+#pragma unroll
+    for (int u = 0; u < kB; ++u) {
+      const uint32_t j = (uint32_t)tid + (uint32_t)u * kFThreads;
+      if (j < nI0 && !((slowI >> u) & 1u)) put_index(bIdx + j, ids_of(ib[u]), t.tlo + sh.u.lst[j]);
+      if (j < nF0 && !((slowF >> u) & 1u)) put_float(j, fb[u], sh.u.lst[fb0 + j], 0, nV0, nL0);
+    }
+  }
+#ifndef FSVM_PF_LATE
+  // the next tile's text loads, in flight through the rest of this tile
+  if (PERSIST && kn < a.ntiles) stage_issue(a.text, a.n, (uint64_t)kn * kTile, sr, bk);
+#endif
+  for (uint32_t p = 0; p < np; ++p) {
+    const uint64_t s = p ? sh.pend[p - 1] : 0, e = p ? sh.pend[p] : pe0;
+    if (p) {  // block-uniform
+      bk.sync();
+      if (mypass == p) build(s, e);
+      bk.sync();
+      slowI = slowF = 0;
+    }
+    const uint64_t cn = e - s;
+    const uint32_t nIp = fI(cn), nVp = fV(cn), nLp = fL(cn), nFp = nVp + nLp + fW(cn), fbp = kIW * nIp;
+    const uint32_t u0 = p ? 0u : (uint32_t)kB;
+    for (uint32_t u = u0, j = (uint32_t)tid + u0 * kFThreads; j < nIp; ++u, j += kFThreads) {
+      const uint32_t o = sh.u.lst[j];
+      bool ok;
+      const uint32_t v = win_index(o, &ok);
+      if (ok) put_index(bIdx + fI(s) + j, ids_of(v), t.tlo + o);
+      slowI |= (ok ? 0u : 1u) << u;
+    }
+    for (uint32_t u = u0, j = (uint32_t)tid + u0 * kFThreads; j < nFp; ++u, j += kFThreads) {
+      const uint32_t o = sh.u.lst[fbp + j];
+      bool ok;
+      const float v = win_float(o, &ok);
+      if (ok) put_float(j, v, o, s, nVp, nLp);
+      slowF |= (ok ? 0u : 1u) << u;
+    }
+    // the byte decoders on the runs the windows left (rare)
+    for (uint32_t m = slowI; m; m &= m - 1) {
+      const uint32_t j = (uint32_t)tid + (uint32_t)ctz32(m) * kFThreads, o = sh.u.lst[j];
+      put_index(bIdx + fI(s) + j, slow_idx(o), t.tlo + o);
+    }
+    for (uint32_t m = slowF; m; m &= m - 1) {
+      const uint32_t j = (uint32_t)tid + (uint32_t)ctz32(m) * kFThreads, o = sh.u.lst[fbp + j];
+      put_float(j, slow_flt(o), o, s, nVp, nLp);
+    }
+    if constexpr (FM)
+      for (uint32_t j = (uint32_t)tid; j < nIp; j += kFThreads) put_field(bIdx + fI(s) + j, sh.u.lst[nIp + j]);
+  }
+  if (imin && one_chunk) {  // block-uniform: one store per wave that saw a 0 id
+    const uint64_t zm = bk.ballot(zero);
+    if ((tid & (kWave - 1)) == 0 && zm) store_flag_u64(&a.umin[sh.c.c_first - 1], 0);
+  }
+  FAST_STAMP(k, 8);
 #ifdef FSVM_PF_LATE
   if (PERSIST && kn < a.ntiles) stage_issue(a.text, a.n, (uint64_t)kn * kTile, sr, bk);
 #endif

@@ -78,6 +78,8 @@ def lib():
             L.dmlc_amd_copy_n.restype = ctypes.c_int
             L.dmlc_amd_copy_n.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p),
                                           ctypes.POINTER(ctypes.c_uint64), ctypes.c_int, ctypes.c_void_p]
+        L.dmlc_amd_fast_geometry.restype = ctypes.c_int
+        L.dmlc_amd_fast_geometry.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]
         L.dmlc_amd_profile_begin.restype = ctypes.c_int
         L.dmlc_amd_profile_end.restype = ctypes.c_int
         L.dmlc_amd_profile_end.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int),
@@ -101,7 +103,15 @@ def profile_end():
 EXPORTED_SYMBOLS = ("dmlc_amd_parse", "dmlc_amd_workspace_bytes", "dmlc_amd_error_string",
                     "dmlc_amd_device_count", "dmlc_amd_abi_version", "dmlc_amd_strtof_batch",
                     "dmlc_amd_profile_begin", "dmlc_amd_profile_end", "dmlc_amd_last_hip_error",
-                    "dmlc_amd_copy", "dmlc_amd_copy_n")
+                    "dmlc_amd_copy", "dmlc_amd_copy_n", "dmlc_amd_fast_geometry")
+
+
+def fast_geometry():
+    """(text bytes per single-pass tile, unit starts one tile takes) of the
+    loaded library (dmlc_amd_fast_geometry)."""
+    t, m = ctypes.c_uint32(0), ctypes.c_uint32(0)
+    lib().dmlc_amd_fast_geometry(ctypes.byref(t), ctypes.byref(m))
+    return int(t.value), int(m.value)
 
 
 def make_params(fmt="libsvm", index_bits=32, value_type="f32", indexing_mode=0, label_column=-1,

@@ -173,6 +173,12 @@ int dmlc_amd_device_count(void);
 /* ABI version this library was built with. */
 int dmlc_amd_abi_version(void);
 
+/* Geometry of the single-pass kernels this library was built with: text
+ * bytes per tile and the most ParseBlock unit starts one tile takes before
+ * the call goes to the exact kernels (diagnostics and tests; either pointer
+ * may be NULL). */
+int dmlc_amd_fast_geometry(uint32_t *tile_bytes, uint32_t *max_unit_starts);
+
 #ifdef __cplusplus
 }
 #endif

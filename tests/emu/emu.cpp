@@ -42,22 +42,33 @@ struct Barrier {
   }
 };
 
-struct BlockCtx {
-  Barrier bar{kThreads};
-  Barrier wbar[kWaves] = {Barrier(kWave), Barrier(kWave), Barrier(kWave), Barrier(kWave)};
-  unsigned char bal[kThreads];
-  uint32_t ws[kThreads];
-  alignas(64) unsigned char scan[kThreads * 64];
-  uint64_t mins[kThreads];
-  uint64_t sh8[kThreads];
+template <int NT>
+struct BlockCtxT {
+  static constexpr int kW = NT / kWave;
+  Barrier bar{NT};
+  std::vector<Barrier *> wbar;
+  unsigned char bal[NT];
+  uint32_t ws[NT];
+  alignas(64) unsigned char scan[NT * 64];
+  uint64_t mins[NT];
+  uint64_t sh8[NT];
+  BlockCtxT() {
+    for (int w = 0; w < kW; ++w) wbar.push_back(new Barrier(kWave));
+  }
+  ~BlockCtxT() {
+    for (auto *b : wbar) delete b;
+  }
 };
 
-struct HostBlock {
+// NT threads per workgroup: kThreads for the exact tiles, fast::kFThreads
+// for the single-pass tiles
+template <int NT>
+struct HostBlockT {
   int t;
-  BlockCtx *ctx;
+  BlockCtxT<NT> *ctx;
   int tid() const { return t; }
   void sync() { ctx->bar.wait(); }
-  void wave_sync() { ctx->wbar[t / kWave].wait(); }
+  void wave_sync() { ctx->wbar[t / kWave]->wait(); }
   uint64_t ballot(bool p) {
     ctx->bal[t] = p;
     wave_sync();
@@ -90,7 +101,7 @@ struct HostBlock {
     ctx->mins[t] = v;
     sync();
     uint64_t r = ~0ull;
-    for (int i = 0; i < kThreads; ++i) r = ctx->mins[i] < r ? ctx->mins[i] : r;
+    for (int i = 0; i < NT; ++i) r = ctx->mins[i] < r ? ctx->mins[i] : r;
     sync();
     return r;
   }
@@ -109,21 +120,23 @@ struct HostBlock {
     T acc = identity;
     for (int i = 0; i < t; ++i) acc = op(acc, buf[i]);
     T all = acc;
-    for (int i = t; i < kThreads; ++i) all = op(all, buf[i]);
+    for (int i = t; i < NT; ++i) all = op(all, buf[i]);
     *total = all;
     sync();
     return acc;
   }
 };
+using HostBlock = HostBlockT<kThreads>;
+using FastBlock = HostBlockT<fast::kFThreads>;
 
-template <typename Body>
+template <int NT = kThreads, typename Body>
 void run_block(Body body) {
-  BlockCtx ctx;
+  BlockCtxT<NT> ctx;
   std::vector<std::thread> th;
-  th.reserve(kThreads);
-  for (int t = 0; t < kThreads; ++t)
+  th.reserve(NT);
+  for (int t = 0; t < NT; ++t)
     th.emplace_back([&, t] {
-      HostBlock bk{t, &ctx};
+      HostBlockT<NT> bk{t, &ctx};
       body(bk);
     });
   for (auto &x : th) x.join();
@@ -261,7 +274,7 @@ extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *c
       for (uint64_t k = 0; k < nft; ++k) {
         fsvm::Shared *sh = new fsvm::Shared;
         std::memset(sh, 0xCD, sizeof(*sh));
-        run_block([&](HostBlock &bk) {
+        run_block<fast::kFThreads>([&](FastBlock &bk) {
           if (fm) {
             if (count_only) fsvm::tile<1, true>(f, *sh, bk, (uint32_t)k);
             else fsvm::tile<2, true>(f, *sh, bk, (uint32_t)k);
@@ -384,12 +397,12 @@ extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *c
         fcsv::Shared *sh = new fcsv::Shared;
         std::memset(sh, 0xCD, sizeof(*sh));
         const bool sp = f.label_col >= 0 || f.weight_col >= 0, iv = f.vtype != 0;
-        if (count_only && iv) run_block([&](HostBlock &bk) { fcsv::tile<1, false, 1>(f, *sh, bk, (uint32_t)k); });
-        else if (iv) run_block([&](HostBlock &bk) { fcsv::tile<2, false, 1>(f, *sh, bk, (uint32_t)k); });
-        else if (count_only && sp) run_block([&](HostBlock &bk) { fcsv::tile<1, true, 0>(f, *sh, bk, (uint32_t)k); });
-        else if (count_only) run_block([&](HostBlock &bk) { fcsv::tile<1, false, 0>(f, *sh, bk, (uint32_t)k); });
-        else if (sp) run_block([&](HostBlock &bk) { fcsv::tile<2, true, 0>(f, *sh, bk, (uint32_t)k); });
-        else run_block([&](HostBlock &bk) { fcsv::tile<2, false, 0>(f, *sh, bk, (uint32_t)k); });
+        if (count_only && iv) run_block<fast::kFThreads>([&](FastBlock &bk) { fcsv::tile<1, false, 1>(f, *sh, bk, (uint32_t)k); });
+        else if (iv) run_block<fast::kFThreads>([&](FastBlock &bk) { fcsv::tile<2, false, 1>(f, *sh, bk, (uint32_t)k); });
+        else if (count_only && sp) run_block<fast::kFThreads>([&](FastBlock &bk) { fcsv::tile<1, true, 0>(f, *sh, bk, (uint32_t)k); });
+        else if (count_only) run_block<fast::kFThreads>([&](FastBlock &bk) { fcsv::tile<1, false, 0>(f, *sh, bk, (uint32_t)k); });
+        else if (sp) run_block<fast::kFThreads>([&](FastBlock &bk) { fcsv::tile<2, true, 0>(f, *sh, bk, (uint32_t)k); });
+        else run_block<fast::kFThreads>([&](FastBlock &bk) { fcsv::tile<2, false, 0>(f, *sh, bk, (uint32_t)k); });
         delete sh;
       }
       if (f.label_col >= 0 || f.weight_col >= 0) {  // label_check_kernel

@@ -262,7 +262,8 @@ def junk_csv(rng, nlines, maxcols=30, delim=",", header=True, violate=False):
                 v = _csv_field(rng)
             if rng.random() < 0.03:
                 v = rng.choice(["nan", "inf", "Infinity", "-inf", "+NAN", "info", " abc", "\xef\xbb\xbf1",
-                                "\t?", " nan", "  -Inf", "nAn", "-nan", "\xe9t\xe9", "in", "na"])
+                                "\t?", " nan", "  -Inf", "nAn", "-nan", "\xe9t\xe9", "in", "na", "infin", "infinit",
+                                "INFINITY", "-Infinity7", "infx", "nana"])
             fields.append(v.replace(delim, ";") if delim != ";" else v.replace(delim, ":"))
         row = delim.join(fields)
         bom = "\xef\xbb\xbf" if rng.random() < 0.05 and row[:1] not in ("", "\r") else ""  # (a BOM ending its line: exact)

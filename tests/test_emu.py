@@ -265,14 +265,18 @@ def test_emu_csv_dense_tokens():
 
 
 def _many_chunks(rng, data, n_cuts, cluster):
-    """Chunk starts after newlines, n_cuts of them; plus a dense cluster (>32
-    starts inside one 16 KiB tile) so both the 64-ary chunk search (nchunk > 64,
-    fast_common.h chunk_list) and the too-many-chunks fallback are exercised."""
+    """Chunk starts after newlines, n_cuts of them; plus a dense cluster (more
+    starts inside one single-pass tile than it takes, kMaxCs) so both the
+    64-ary chunk search (nchunk > 64, fast_common.h chunk_list) and the
+    too-many-chunks fallback are exercised."""
+    import dmlc_amd
+    tile, max_cs = dmlc_amd.fast_geometry()
     a = np.frombuffer(data, dtype=np.uint8)
     nl = (np.flatnonzero(a == 10) + 1)
     nl = nl[nl < len(data)]
     cuts = set(rng.choice(nl, size=min(n_cuts, len(nl)), replace=False).tolist())
-    mid = nl[(nl > 20000) & (nl < 36000)][:40]  # a cluster in tiles 1-2
+    mid = nl[(nl > 2 * tile) & (nl < 3 * tile)]  # a cluster in tile 2
+    assert len(mid) > max_cs
     if cluster:
         cuts |= set(mid.tolist())
     return [0] + sorted(cuts) + [len(data)]

@@ -590,8 +590,8 @@ def test_gpu_config5_shards_vs_oracle(dm):
 @pytest.mark.parametrize("fmt", [po.LIBSVM, po.CSV])
 def test_gpu_fast_many_chunks_vs_oracle(dm, fmt):
     """Hundreds to thousands of chunks: the 64-ary chunk search of every tile
-    (fast_common.h chunk_list, 1-3 load rounds) and a >32-starts cluster that
-    sends the input to the exact kernels."""
+    (fast_common.h chunk_list, 1-3 load rounds) and a cluster of more starts
+    than one tile takes (kMaxCs) that sends the input to the exact kernels."""
     rng = np.random.default_rng(5150)
     if fmt == po.LIBSVM:
         text, _ = synth.rows(synth.LIBSVM, 20000, 24, seed=8)
@@ -602,17 +602,18 @@ def test_gpu_fast_many_chunks_vs_oracle(dm, fmt):
     nl = np.flatnonzero(a == 10) + 1
     nl = nl[nl < len(data)]
     name = FMT_NAME[fmt]
+    tile, max_cs = dm.fast_geometry()
     for n_cuts, cluster in ((65, False), (600, False), (5000, False), (600, True)):
         cuts = set(rng.choice(nl, size=min(n_cuts, len(nl)), replace=False).tolist())
         if cluster:
-            cuts |= set(nl[(nl > 32868) & (nl < 49052)].tolist())  # one tile
+            cuts |= set(nl[(nl > 2 * tile + 100) & (nl < 3 * tile - 100)].tolist())  # one tile
         offs = [0] + sorted(cuts) + [len(data)]
         st = np.asarray(offs[:-1])  # chunk starts a tile lists: tlo <= s <= thi (fast_common.h)
-        tl = np.arange(0, len(data), 16384)
-        per_tile = int((np.searchsorted(st, np.minimum(tl + 16384, len(data)), "right")
+        tl = np.arange(0, len(data), tile)
+        per_tile = int((np.searchsorted(st, np.minimum(tl + tile, len(data)), "right")
                         - np.searchsorted(st, tl, "left")).max())
         h = _oracle_vs_gpu(dm, data, offs, fmt)
-        assert h["path"] == ("exact" if per_tile > 32 else "fast"), (name, n_cuts, per_tile, h["path"])
+        assert h["path"] == ("exact" if per_tile > max_cs else "fast"), (name, n_cuts, per_tile, h["path"])
 
 
 @pytest.mark.gpu
