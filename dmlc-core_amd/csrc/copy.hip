@@ -72,8 +72,79 @@ __global__ void __launch_bounds__(kCopyThreads) copy_n_kernel(CopyList L) {
   if (b + 1 == nb && threadIdx.x < tail)
     reinterpret_cast<uint8_t *>(dst + n16)[threadIdx.x] = reinterpret_cast<const uint8_t *>(src + n16)[threadIdx.x];
 }
+
+// Device-sized form: copy i's byte count comes from d_counts when the kernel
+// runs (its blocks were laid out for max_bytes; the ones past the count idle)
+struct CopyListDev {
+  uint4 *dst[kCopyN];
+  const uint4 *src[kCopyN];
+  uint64_t scale[kCopyN], add[kCopyN], maxb[kCopyN];
+  int slot[kCopyN];
+  uint32_t first[kCopyN + 1];
+  int n;
+};
+__global__ void __launch_bounds__(kCopyThreads) copy_n_dev_kernel(CopyListDev L, const uint64_t *d_counts) {
+  int i = 0;
+  while (i + 1 < L.n && blockIdx.x >= L.first[i + 1]) ++i;  // block-uniform
+  const uint32_t b = blockIdx.x - L.first[i], nb = L.first[i + 1] - L.first[i];
+  uint64_t bytes = L.slot[i] >= 0 ? d_counts[L.slot[i]] * L.scale[i] + L.add[i] : L.add[i];
+  bytes = bytes < L.maxb[i] ? bytes : L.maxb[i];
+  uint4 *__restrict__ dst = L.dst[i];
+  const uint4 *__restrict__ src = L.src[i];
+  const uint64_t n16 = bytes >> 4;
+  const uint64_t stride = (uint64_t)nb * kCopyThreads * kCopyUnroll;
+  for (uint64_t j0 = (uint64_t)b * kCopyThreads * kCopyUnroll + threadIdx.x; j0 < n16; j0 += stride) {
+    uint4 v[kCopyUnroll];
+#pragma unroll
+    for (int u = 0; u < kCopyUnroll; ++u) {
+      const uint64_t j = j0 + (uint64_t)u * kCopyThreads;
+      if (j < n16) v[u] = src[j];
+    }
+#pragma unroll
+    for (int u = 0; u < kCopyUnroll; ++u) {
+      const uint64_t j = j0 + (uint64_t)u * kCopyThreads;
+      if (j < n16) dst[j] = v[u];
+    }
+  }
+  const uint32_t tail = (uint32_t)(bytes & 15u);
+  if (b == 0 && threadIdx.x < tail)
+    reinterpret_cast<uint8_t *>(dst + n16)[threadIdx.x] = reinterpret_cast<const uint8_t *>(src + n16)[threadIdx.x];
+}
 }  // namespace
 }  // namespace dmlc_amd
+
+extern "C" int dmlc_amd_copy_n_dev(void *const *dst, const void *const *src, const uint64_t *d_counts,
+                                   const int *slot, const uint64_t *scale, const uint64_t *add,
+                                   const uint64_t *max_bytes, int n, void *stream) {
+  if (n < 0 || n > DMLC_AMD_COPY_MAX || (n && (!dst || !src || !slot || !scale || !add || !max_bytes)))
+    return DMLC_AMD_ERR_ARG;
+  const hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  dmlc_amd::CopyListDev L;
+  L.n = 0;
+  uint32_t blocks = 0;
+  const uint64_t per_block = (uint64_t)dmlc_amd::kCopyThreads * dmlc_amd::kCopyUnroll;
+  for (int i = 0; i < n; ++i) {
+    if (max_bytes[i] == 0) continue;
+    if (!dst[i] || !src[i] || (slot[i] >= 0 && !d_counts)) return DMLC_AMD_ERR_ARG;
+    if (((reinterpret_cast<uintptr_t>(dst[i]) | reinterpret_cast<uintptr_t>(src[i])) & 15u) != 0)
+      return DMLC_AMD_ERR_ARG;
+    const uint64_t nb =
+        std::max<uint64_t>(1, std::min<uint64_t>(((max_bytes[i] >> 4) + per_block - 1) / per_block, 1024));
+    L.dst[L.n] = static_cast<uint4 *>(dst[i]);
+    L.src[L.n] = static_cast<const uint4 *>(src[i]);
+    L.slot[L.n] = slot[i];
+    L.scale[L.n] = scale[i];
+    L.add[L.n] = add[i];
+    L.maxb[L.n] = max_bytes[i];
+    L.first[L.n] = blocks;
+    blocks += (uint32_t)nb;
+    ++L.n;
+  }
+  if (L.n == 0) return DMLC_AMD_OK;
+  L.first[L.n] = blocks;
+  dmlc_amd::copy_n_dev_kernel<<<blocks, dmlc_amd::kCopyThreads, 0, s>>>(L, d_counts);
+  return hipGetLastError() == hipSuccess ? DMLC_AMD_OK : DMLC_AMD_ERR_HIP;
+}
 
 extern "C" int dmlc_amd_copy_n(void *const *dst, const void *const *src, const uint64_t *bytes, int n,
                                void *stream) {

@@ -350,7 +350,11 @@ struct EngineConfig {
   // gathered on the device into one D2H copy 18 GB/s -- although the SDMA
   // engines run both directions of 1 GiB copies at 97 GB/s together,
   // tools/e2e/link_probe.py)
-  enum CopyMode { kKernel, kDma } copy_mode = kKernel;
+  // "h2d_kernel" / "d2h_kernel": one direction by kernel, the other by DMA
+  // (the SDMA engines and the copy kernels then carry different directions).
+  enum CopyMode { kKernel, kDma, kH2DKernel, kD2HKernel } copy_mode = kKernel;
+  bool h2d_kernel() const { return copy_mode == kKernel || copy_mode == kH2DKernel; }
+  bool d2h_kernel() const { return copy_mode == kKernel || copy_mode == kD2HKernel; }
 
   // batch size, devices and workers from the environment
   // (DMLC_AMD_BATCH_BYTES, DMLC_AMD_DEVICES = "0,1,..." | "all", DMLC_AMD_WORKERS)
@@ -360,8 +364,11 @@ struct EngineConfig {
     if (const char *st = std::getenv("DMLC_AMD_STATS")) stats = std::atoi(st) != 0;
     if (const char *c = std::getenv("DMLC_AMD_COPY")) {
       const std::string v(c);
-      if (v != "dma" && v != "kernel") throw dmlc::Error("DMLC_AMD_COPY: expected kernel or dma, got " + v);
-      copy_mode = v == "kernel" ? kKernel : kDma;
+      if (v == "kernel") copy_mode = kKernel;
+      else if (v == "dma") copy_mode = kDma;
+      else if (v == "h2d_kernel") copy_mode = kH2DKernel;
+      else if (v == "d2h_kernel") copy_mode = kD2HKernel;
+      else throw dmlc::Error("DMLC_AMD_COPY: expected kernel, dma, h2d_kernel or d2h_kernel, got " + v);
     }
     if (const char *d = std::getenv("DMLC_AMD_DEVICES")) {
       devices.clear();
@@ -469,6 +476,7 @@ class HipTextParser : public dmlc::Parser<IndexType, DType> {
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};  // stats: H2D | parse | D2H boundaries
     DevBuf text, cs, res, tab, ws, off, label, weight, qid, index, field, value;
     uint64_t cap[7] = {0, 0, 0, 0, 0, 0, 0};
+    uint64_t est[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // copy-out bytes per CSR array, from earlier batches
     PinnedVec<dmlc_amd_result> hres;
   };
 
@@ -655,10 +663,37 @@ class HipTextParser : public dmlc::Parser<IndexType, DType> {
     uint64_t want[7];
     for (int i = 0; i < 7; ++i) want[i] = std::max<uint64_t>(w->cap[i], ub);
     dmlc_amd_csr out;
+    // The CSR copy-out by kernel is queued right behind the parse with its
+    // sizes read on the device (dmlc_amd_copy_n_dev), into host arrays sized
+    // from the worker's earlier batches: no host round trip between the parse
+    // and the copy.  A batch larger than the estimate copies again after the
+    // sync with its exact sizes.
+    const size_t isz = sizeof(IndexType), dsz = sizeof(DType);
+    const int kSlot[8] = {DMLC_AMD_ROWS, DMLC_AMD_LABEL, DMLC_AMD_WEIGHT, DMLC_AMD_QID,
+                          DMLC_AMD_INDEX, DMLC_AMD_FIELD, DMLC_AMD_VALUE, -1};
+    const uint64_t kScale[8] = {8, dsz, 4, 8, isz, isz, dsz, 0};
+    const uint64_t kAdd[8] = {8, 0, 0, 0, 0, 0, 0, (uint64_t)nunits * 64};
+    bool pre = false;  // the copy-out went with the parse
+    uint64_t pre_max[8];
+    void *pre_dst[8];
     for (int attempt = 0;; ++attempt) {
       Outputs(w, want, &out);
       CheckRc(dmlc_amd_parse(d_text, b->bytes, d_cs, nch, &p, &out, d_tab, d_ws, ws,
                              reinterpret_cast<dmlc_amd_result *>(d_res), s));
+      pre = attempt == 0 && cfg_.d2h_kernel() && w->est[0] > 0;
+      if (pre) {
+        const void *src[8] = {out.offset, out.label, out.weight, out.qid, out.index, out.field, out.value, d_tab};
+        pre_dst[0] = b->off.reserve(w->est[0] / 8 + 1);
+        pre_dst[1] = b->label.reserve(w->est[1] / dsz + 1);
+        pre_dst[2] = b->weight.reserve(w->est[2] / 4 + 1);
+        pre_dst[3] = b->qid.reserve(w->est[3] / 8 + 1);
+        pre_dst[4] = b->index.reserve(w->est[4] / isz + 1);
+        pre_dst[5] = b->field.reserve(w->est[5] / isz + 1);
+        pre_dst[6] = b->value.reserve(w->est[6] / dsz + 1);
+        pre_dst[7] = b->tab.reserve(nunits * 8);
+        for (int i = 0; i < 8; ++i) pre_max[i] = i == 7 ? (uint64_t)nunits * 64 : w->est[i];
+        CheckRc(dmlc_amd_copy_n_dev(pre_dst, src, d_res, kSlot, kScale, kAdd, pre_max, 8, s));
+      }
       hip_check(hipMemcpyAsync(hres, d_res, sizeof(dmlc_amd_result), hipMemcpyDeviceToHost, s), "D2H result");
       if (st) hip_check(hipEventRecord(w->ev[2], s), "hipEventRecord");
       hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
@@ -688,11 +723,18 @@ class HipTextParser : public dmlc::Parser<IndexType, DType> {
                     b->weight.reserve(c[DMLC_AMD_WEIGHT] + 1), b->qid.reserve(c[DMLC_AMD_QID] + 1),
                     b->index.reserve(c[DMLC_AMD_INDEX] + 1), b->field.reserve(c[DMLC_AMD_FIELD] + 1),
                     b->value.reserve(c[DMLC_AMD_VALUE] + 1), b->tab.reserve(nunits * 8)};
-    if (cfg_.copy_mode == EngineConfig::kKernel) CheckRc(dmlc_amd_copy_n(dst, src, nb, 8, s));
-    else
-      for (int i = 0; i < 8; ++i) D2H(dst[i], src[i], nb[i], s);
+    bool again = !pre;
+    for (int i = 0; i < 8; ++i) {
+      again = again || nb[i] > pre_max[i] || (nb[i] && dst[i] != pre_dst[i]);
+      w->est[i] = std::max<uint64_t>(w->est[i], (nb[i] + nb[i] / 4 + 4095) & ~uint64_t(15));
+    }
+    if (again) {
+      if (cfg_.d2h_kernel()) CheckRc(dmlc_amd_copy_n(dst, src, nb, 8, s));
+      else
+        for (int i = 0; i < 8; ++i) D2H(dst[i], src[i], nb[i], s);
+    }
     if (st) hip_check(hipEventRecord(w->ev[3], s), "hipEventRecord");
-    hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
+    if (again) hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
     const Clock clk;
     BuildBlocks(b, nunits, upc);
     if (st) {
@@ -710,12 +752,12 @@ class HipTextParser : public dmlc::Parser<IndexType, DType> {
   // (dmlc_amd_copy) unless DMLC_AMD_COPY=dma
   void H2D(void *dst, const void *src, size_t bytes, hipStream_t s) {
     if (!bytes) return;
-    if (cfg_.copy_mode == EngineConfig::kKernel) CheckRc(dmlc_amd_copy(dst, src, bytes, s));
+    if (cfg_.h2d_kernel()) CheckRc(dmlc_amd_copy(dst, src, bytes, s));
     else hip_check(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s), "H2D");
   }
   void D2H(void *dst, const void *src, size_t bytes, hipStream_t s) {
     if (!bytes) return;
-    if (cfg_.copy_mode == EngineConfig::kKernel) CheckRc(dmlc_amd_copy(dst, src, bytes, s));
+    if (cfg_.d2h_kernel()) CheckRc(dmlc_amd_copy(dst, src, bytes, s));
     else hip_check(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s), "D2H");
   }
 

@@ -103,7 +103,7 @@ def profile_end():
 EXPORTED_SYMBOLS = ("dmlc_amd_parse", "dmlc_amd_workspace_bytes", "dmlc_amd_error_string",
                     "dmlc_amd_device_count", "dmlc_amd_abi_version", "dmlc_amd_strtof_batch",
                     "dmlc_amd_profile_begin", "dmlc_amd_profile_end", "dmlc_amd_last_hip_error",
-                    "dmlc_amd_copy", "dmlc_amd_copy_n", "dmlc_amd_fast_geometry")
+                    "dmlc_amd_copy", "dmlc_amd_copy_n", "dmlc_amd_copy_n_dev", "dmlc_amd_fast_geometry")
 
 
 def fast_geometry():

@@ -153,6 +153,16 @@ int dmlc_amd_copy(void *dst, const void *src, uint64_t bytes, void *stream);
 #define DMLC_AMD_COPY_MAX 16
 int dmlc_amd_copy_n(void *const *dst, const void *const *src, const uint64_t *bytes, int n, void *stream);
 
+/* The same with sizes known only on the device (a parse's result counts, so
+ * the copy-out needs no host round trip after the parse): copy i moves
+ * min(max_bytes[i], d_counts[slot[i]] * scale[i] + add[i]) bytes, or add[i]
+ * when slot[i] < 0.  d_counts is read on the device when the copy runs;
+ * slot / scale / add / max_bytes are host arrays of n entries.  All pairs
+ * must be 16-byte aligned. */
+int dmlc_amd_copy_n_dev(void *const *dst, const void *const *src, const uint64_t *d_counts, const int *slot,
+                        const uint64_t *scale, const uint64_t *add, const uint64_t *max_bytes, int n,
+                        void *stream);
+
 /* Kernel timing for benchmarks: between profile_begin and profile_end, every
  * dmlc_amd_parse on this thread brackets its dominant kernel (the single-pass
  * kernel, or the exact write kernel) with HIP events on its stream.

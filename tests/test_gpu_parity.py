@@ -796,6 +796,38 @@ def test_gpu_kernel_copy_n(dm):
     assert L.dmlc_amd_copy_n(dp, sp, nb, 17, s) != 0  # more than DMLC_AMD_COPY_MAX
 
 
+def test_gpu_kernel_copy_n_dev(dm):
+    """dmlc_amd_copy_n_dev (the engine's copy-out queued behind the parse):
+    sizes count * scale + add read on the device, clamped at max_bytes,
+    constant sizes for slot < 0, nothing written past a size."""
+    import ctypes
+    import torch
+    L = dm.lib()
+    L.dmlc_amd_copy_n_dev.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                      ctypes.c_void_p]
+    rng = np.random.default_rng(6)
+    counts = torch.tensor([300001, 0, 7, 2_000_003, 5, 9, 11, 1], dtype=torch.int64, device="cuda")
+    slot = [0, 1, 2, 3, 4, -1, 6, 7]
+    scale = [8, 4, 1, 4, 16, 0, 4, 4]
+    add = [8, 0, 6, 0, 0, 4096, 0, 0]
+    maxb = [8 * 300002 + 64, 64, 64, 4 * 2_000_003 + 64, 48, 5000, 40, 64]  # entries 4 and 6 clamp
+    c = counts.cpu().numpy()
+    want = [min(maxb[i], (int(c[slot[i]]) * scale[i] + add[i]) if slot[i] >= 0 else add[i]) for i in range(8)]
+    srcs = [torch.from_numpy(rng.integers(0, 256, m + 32, dtype=np.uint8)).cuda() for m in maxb]
+    dsts = [torch.zeros(m + 32, dtype=torch.uint8).pin_memory() for m in maxb]
+    arr = lambda t, v: (t * len(v))(*v)  # noqa: E731
+    rc = L.dmlc_amd_copy_n_dev(arr(ctypes.c_void_p, [d.data_ptr() for d in dsts]),
+                               arr(ctypes.c_void_p, [x.data_ptr() for x in srcs]), counts.data_ptr(),
+                               arr(ctypes.c_int, slot), arr(ctypes.c_uint64, scale), arr(ctypes.c_uint64, add),
+                               arr(ctypes.c_uint64, maxb), 8, torch.cuda.current_stream().cuda_stream)
+    assert rc == 0
+    torch.cuda.synchronize()
+    for n, x, d in zip(want, srcs, dsts):
+        assert torch.equal(d[:n], x[:n].cpu()), n
+        assert int(d[n:].sum()) == 0, n
+
+
 @pytest.mark.parametrize("fmt", [po.LIBSVM, po.LIBFM])
 def test_gpu_qid_letter_forms_vs_oracle(dm, fmt):
     """Letters of "qid" that spell no "qid:" token leave the single-pass

@@ -37,7 +37,8 @@ def main():
     counts = p.count(d_text, d_cs, result=res)
     out = p.alloc(counts)
     out["_csr"] = p.csr_of(out)
-    ntiles = (text.size + 16383) // 16384
+    tile, _ = dmlc_amd.fast_geometry()
+    ntiles = (text.size + tile - 1) // tile
     n = min(ntiles, 1 << 17)
     for mode in ("count", "full"):
         for _ in range(3):
