@@ -295,6 +295,7 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
     if (m.hi) {  // bytes >= 0x80 (rare): their classes byte by byte (junk, a delimiter, or outside)
       const uint8_t *seg = sh.c.text + kPre + tid * kSegB;
       const uint64_t h = hi_mask64(seg);
+      m = classify64_lut<true>(seg, sh.cls);
       m.d &= ~h;
       m.g &= ~h;
       m.n &= ~h;

@@ -78,17 +78,12 @@ struct Masks {
 
 // The class tables hold the 128 ASCII bytes (512 bytes of LDS per tile); a
 // byte >= 0x80 still indexes by its value -- on the device the read lands in
-// the tile's next LDS arrays, and its planes are replaced afterwards (Masks.hi,
-// hi_mask64): the index stays one SDWA shift.  Host builds (the emulator) mask
-// the index instead.
+// the tile's next LDS arrays (the Shared layouts put DecTables there), and its
+// planes are replaced afterwards (Masks.hi, hi_mask64): the index stays one
+// SDWA shift.  The emulator builds the same Shared structs and reads the same
+// words, so it sees what the device sees.
 constexpr int kClsEntries = 128;
-DA_HD uint32_t cls_index(uint32_t b) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  return b & 0xFFu;
-#else
-  return b & 0x7Fu;
-#endif
-}
+DA_HD uint32_t cls_index(uint32_t b) { return b & 0xFFu; }
 // bit i: byte i of the 64 at p (16-byte aligned) is >= 0x80 (rare: a slow loop)
 DA_HD uint64_t hi_mask64(const uint8_t *p) {
   uint64_t m = 0;
@@ -194,7 +189,12 @@ DA_HD uint32_t class_of(uint32_t b) {
   return 0x00000100u;
 }
 
-// Masks of the 64 bytes at p (16-byte aligned) through the class table.
+// Masks of the 64 bytes at p (16-byte aligned) through the class table.  On
+// the device a byte >= 0x80 reads a word past the table whose bits, shifted
+// into the plane bytes, can land on the planes of the other bytes of its
+// 8-byte group: a segment with m.hi must be classified again with kAscii
+// (index & 0x7F, every entry a table class) before its planes are used.
+template <bool kAscii = false>
 DA_HD Masks classify64_lut(const uint8_t *p, const uint32_t *cls) {
   uint32_t acc[8];
   uint32_t orv = 0;
@@ -208,7 +208,7 @@ DA_HD Masks classify64_lut(const uint8_t *p, const uint32_t *cls) {
 #pragma unroll
       for (int b = 0; b < 4; ++b) {
         const int i = 16 * q + 4 * j + b;
-        const uint32_t x = cls[cls_index((w[j] >> (8 * b)) & 0xFFu)];
+        const uint32_t x = cls[kAscii ? (w[j] >> (8 * b)) & 0x7Fu : cls_index((w[j] >> (8 * b)) & 0xFFu)];
         if ((i & 7) == 0) acc[i >> 3] = x;
         else acc[i >> 3] |= x << (i & 7);
       }
@@ -237,11 +237,12 @@ DA_HD Masks classify64_lut(const uint8_t *p, const uint32_t *cls) {
   return m;
 }
 // 4 bytes (x) through the table: 4-bit masks (a byte >= 0x80: r.hi, planes
-// cleared, bad)
+// cleared, bad; its table word is masked to the plane bits so that it cannot
+// reach the other bytes' planes)
 DA_HD Nib classify_dword_lut(uint32_t x, const uint32_t *cls) {
   uint32_t acc = 0;
 #pragma unroll
-  for (int b = 0; b < 4; ++b) acc |= cls[cls_index((x >> (8 * b)) & 0xFFu)] << b;
+  for (int b = 0; b < 4; ++b) acc |= (cls[cls_index((x >> (8 * b)) & 0xFFu)] & 0x01010101u) << b;
   const uint32_t h = hi_nib4(x), k = ~h & 0xFu;
   Nib r;
   r.d = acc & k;

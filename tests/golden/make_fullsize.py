@@ -39,9 +39,26 @@ CONFIGS = {
     "libsvm_1m_x128": (synth.LIBSVM, po.LIBSVM, 1 << 20, 128, 0),
     "csv_1m_x256": (synth.CSV, po.CSV, 1 << 20, 256, 0),
     "libsvm_1m_x2048": (synth.LIBSVM, po.LIBSVM, 1 << 20, 2048, 0),
+    # the bench's grammar / parameter variants of configs 2 and 3 (bench.py CONFIGS)
+    "libsvm_nt2_1m_x128": (synth.LIBSVM, po.LIBSVM, 1 << 20, 128, 0),
+    "libsvm_exact_1m_x128": (synth.LIBSVM, po.LIBSVM, 1 << 20, 128, 0),
+    "csv_exact_1m_x256": (synth.CSV, po.CSV, 1 << 20, 256, 0),
+    "csv_nan_1m_x256": (synth.CSV_NAN, po.CSV, 1 << 20, 256, 0),
+    "libsvm_qid_1m_x128": (synth.LIBSVM_QID, po.LIBSVM, 1 << 20, 128, 0),
+    "libsvm_cmt_1m_x128": (synth.LIBSVM_CMT, po.LIBSVM, 1 << 20, 128, 0),
+    "libsvm_1b_im1_1m_x128": (synth.LIBSVM_1B, po.LIBSVM, 1 << 20, 128, 0),
+    "libfm_1m_x64": (synth.LIBFM, po.LIBFM, 1 << 20, 64, 0),
 }
 for _r in range(8):  # config 5: bench.py's rank r shard of 32M x 64 (4M rows from row r * 4M)
     CONFIGS["libsvm_32m_x64_part%d" % _r] = (synth.LIBSVM, po.LIBSVM, 4 << 20, 64, _r * (4 << 20))
+# parser arguments (the reference's URI args) per config, for the reference
+# and the GPU alike; FLAGS: GPU-only dmlc_amd_params.flags (the result must not
+# depend on them) and the path the GPU must report (0 single pass, 1 exact)
+PARAMS = {
+    "libsvm_nt2_1m_x128": {"nthread": 2},
+    "libsvm_1b_im1_1m_x128": {"indexing_mode": -1},
+}
+FLAGS = {"libsvm_exact_1m_x128": ("exact", 1), "csv_exact_1m_x256": ("exact", 1)}
 
 
 def stream_chunks(sfmt, rows, width, row0, block_rows):
@@ -79,13 +96,14 @@ def stream_chunks(sfmt, rows, width, row0, block_rows):
         del buf[:e]
 
 
-def parse_batch(chunks, ofmt):
+def parse_batch(chunks, ofmt, kw):
     offs = np.cumsum([0] + [len(c) for c in chunks]).tolist()
-    return po.ref_parse_chunks(b"".join(chunks), offs, fmt=ofmt)
+    return po.ref_parse_chunks(b"".join(chunks), offs, fmt=ofmt, **kw)
 
 
 def run(name):
     sfmt, ofmt, rows, width, row0 = CONFIGS[name]
+    kw = PARAMS.get(name, {})
     block_rows = max(1, (16 << 20) // (width * 16))
     hs = {k: hashlib.sha256() for k in ARRAYS}
     sizes = {k: 0 for k in ARRAYS}
@@ -117,12 +135,12 @@ def run(name):
             nchunks += 1
             batch.append(ch)
             if len(batch) == 4:
-                pending.append(ex.submit(parse_batch, batch, ofmt))
+                pending.append(ex.submit(parse_batch, batch, ofmt, kw))
                 batch = []
             while len(pending) > 12 or (pending and pending[0].done()):
                 consume(pending.pop(0).result())
         if batch:
-            pending.append(ex.submit(parse_batch, batch, ofmt))
+            pending.append(ex.submit(parse_batch, batch, ofmt, kw))
         for f in pending:
             consume(f.result())
     if sizes["offset"] == 0:
@@ -130,7 +148,8 @@ def run(name):
         sizes["offset"] = 1
     res = {"format": {po.LIBSVM: "libsvm", po.CSV: "csv", po.LIBFM: "libfm"}[ofmt], "rows": rows,
            "width": width, "row0": row0, "seed": 1, "input_bytes": nbytes, "chunks": nchunks,
-           "first_chunk_sha256": first_chunk_sha, "reference": "oracle/_ref (genuine ParseBlock, nthread 1)",
+           "first_chunk_sha256": first_chunk_sha, "reference": "oracle/_ref (genuine ParseBlock, nthread %d)" % kw.get("nthread", 1),
+           "params": kw,
            "sha256": {k: hs[k].hexdigest() for k in ARRAYS}, "sizes": sizes}
     print("%s: %.2f GB, %d chunks, %d rows, %d entries in %.0f s" % (name, nbytes / 1e9, nchunks,
                                                                         sizes["offset"] - 1, sizes["index"],

@@ -963,8 +963,10 @@ FULL = load_json("synth_full.json") if __import__("os").path.exists(
 @pytest.mark.parametrize("name", sorted(FULL))
 def test_gpu_fullsize_vs_reference_hashes(dm, name):
     """BASELINE configs 2-5 at full size (config 5: each of bench.py's 8
-    per-rank shards), generated and chunked exactly as the bench does, parsed
-    on the GPU's default path, every output array hashed and compared with the
+    per-rank shards) and the bench's variants of configs 2 / 3 (nthread 2,
+    the exact kernels, nan fields + BOM, qid, comments, 1-based ids with
+    indexing_mode -1, libfm), generated and chunked exactly as the bench does,
+    parsed on the GPU with the bench's parameters, every output array hashed and compared with the
     SHA-256 the GENUINE reference's ParseBlock produced for the same chunks
     (tests/golden/make_fullsize.py, oracle/_ref).  The text streams to the
     device chunk by chunk and the arrays stream back in slices, so host memory
@@ -986,10 +988,11 @@ def test_gpu_fullsize_vs_reference_hashes(dm, name):
         starts.append(pos)
     assert pos == fx["input_bytes"] and len(starts) - 1 == fx["chunks"]
     d_cs = torch.tensor(starts, dtype=torch.int64, device="cuda")
-    p = dm.DeviceParser(fx["format"])
+    flags, want_path = mf.FLAGS.get(name, (None, 0))
+    p = dm.DeviceParser(fx["format"], flags=dm.FLAG_EXACT if flags == "exact" else 0, **mf.PARAMS.get(name, {}))
     out = p.parse(d_text, d_cs)
     del d_text
-    assert out["error"] == 0 and out["path"] == 0, (out["error"], out["path"])
+    assert out["error"] == 0 and out["path"] == want_path, (out["error"], out["path"])
     c = out["counts"]
     for k, slot in (("offset", dm.ROWS), ("label", dm.LABEL), ("weight", dm.WEIGHT), ("qid", dm.QID),
                     ("field", dm.FIELD), ("index", dm.INDEX), ("value", dm.VALUE)):

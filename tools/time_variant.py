@@ -15,7 +15,10 @@ from tools import synth  # noqa: E402
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "libsvm"
 fmt, rows, width, kind = {"libsvm": ("libsvm", 1 << 20, 128, synth.LIBSVM), "csv": ("csv", 1 << 20, 256, synth.CSV),
-                          "qid": ("libsvm", 1 << 20, 128, synth.LIBSVM_QID)}[cfg]
+                          "qid": ("libsvm", 1 << 20, 128, synth.LIBSVM_QID),
+                          "cmt": ("libsvm", 1 << 20, 128, synth.LIBSVM_CMT),
+                          "libfm": ("libfm", 1 << 20, 64, synth.LIBFM),
+                          "csv_nan": ("csv", 1 << 20, 256, synth.CSV_NAN)}[cfg]
 text, _ = synth.rows(kind, rows, width, seed=1)
 starts = dmlc_amd.text_chunk_starts(text)
 dev = torch.device("cuda", 0)
