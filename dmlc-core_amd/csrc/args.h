@@ -82,12 +82,14 @@ struct FastSvmArgs {
 // the persistent launch's ticket word follows them
 constexpr uint64_t kFastLbWords = 5;
 
-// Threads of a single-pass tile (fast_common.h): one wave by default -- a
-// tile's phases then need no barrier between waves and the tiles on a CU
-// hide each other's latencies independently; 256 (four waves, 16 KiB
-// tiles) is the round-3 geometry, kept buildable for A/B timing.
+// Threads of a single-pass tile (fast_common.h): four waves, 16 KiB tiles.
+// One wave per tile (4 KiB tiles, no barriers between waves, -DFAST_THREADS=64)
+// and two (128) stay buildable for A/B timing; on MI355X they measured
+// 3.90 / 2.25 ms against 1.78 ms on config 2 (gpurun_out/ab_r4f.txt: per wave
+// VALU 2725 / 1961 / 1709 -- the tile-level work of the look-back, the unit
+// search and the run-list rounds does not shrink with the tile).
 #ifndef FAST_THREADS
-#define FAST_THREADS 64
+#define FAST_THREADS 256
 #endif
 constexpr int kFastThreads = FAST_THREADS;
 constexpr uint64_t kFastTileBytes = (uint64_t)kFastThreads * 64;  // 64 text bytes per thread

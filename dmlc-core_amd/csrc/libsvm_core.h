@@ -19,6 +19,7 @@
 #pragma once
 #include "args.h"
 #include "decode.h"
+#include "fast_common.h"
 
 namespace dmlc_amd {
 namespace svm {
@@ -108,7 +109,67 @@ struct Shared {  // LDS of one workgroup
   uint8_t win[kWin + 32];
   uint32_t r1bits[kWin / 32 + 1];
   uint64_t pending[2];  // R1 of a line whose head crossed a window, by window parity
+  fast::DecTables dt;   // the window decoders' tables (fast_common.h)
 };
+
+// The 16 bytes at x from the staged window (two aligned LDS words per output
+// word, funnel-shifted), when all of them lie inside the window and before
+// the chunk end: the run at x can then be decoded in registers by the
+// window decoders of the single-pass kernels (fast_common.h wfloat32 /
+// wuint32), which report when the run does not fit their form -- the byte
+// decoders of decode.h take those.
+DA_HD bool win16(const Src &s, uint64_t x, uint32_t w[4]) {
+  if (x < s.wbase || x + 16 > s.wend || x + 16 > s.lim) return false;
+  const uint64_t o = x - s.wbase;
+  const uint32_t *q = reinterpret_cast<const uint32_t *>(s.lds + (o & ~3ull));
+  const uint32_t sh = 8u * (uint32_t)(o & 3u);
+  uint32_t v[5];
+  for (int i = 0; i < 5; ++i) v[i] = q[i];
+  for (int i = 0; i < 4; ++i) w[i] = fast::funnel(v[i + 1], v[i], sh);
+  return true;
+}
+// bit i: window byte i is not '0'..'9' -- any byte value (fast_common.h nd4
+// assumes bytes < 0x80, which the single-pass grammar guarantees and the
+// text of the exact kernels does not)
+DA_HD uint32_t nondigit16(const uint32_t w[4]) {
+  uint32_t m = 0;
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t y = w[i] & 0x7F7F7F7Fu;
+    const uint32_t t = ((((y ^ 0x30303030u) + 0x76767676u) | w[i]) >> 7) & 0x01010101u;
+    m |= fast::udot4(t, 0x08040201u, 0u) << (4 * i);
+  }
+  return m;
+}
+// ParseUnsignedInt of the run at x through the window when it fits (a '-' or
+// more than 8 digits: the byte decoder, which also raises the '-' error)
+DA_HD bool index_at(const Src &src, uint64_t x, bool wide, const fast::DecTables *dt, uint64_t *v) {
+  uint32_t w[4];
+  if (dt && win16(src, x, w)) {
+    bool ok;
+    uint64_t t;
+    const bool pos = fast::wuint32m(w, nondigit16(w), *dt, &t, &ok);
+    if (ok && pos) {
+      *v = t;
+      return true;
+    }
+  }
+  return parse_uint(src, x, wide, v);
+}
+// ParseFloat<float> of the run at x through the window when it fits.  Beyond
+// the single-pass grammar, a sign followed by inf / nan letters is left to
+// the byte decoder (wfloat32 reads it as a signed zero).
+DA_HD float value_at(const Src &src, uint64_t x, const fast::DecTables *dt, bool *nan_err) {
+  uint32_t w[4];
+  if (dt && win16(src, x, w)) {
+    const uint32_t b0 = w[0] & 0xFFu, b1 = ((w[0] >> 8) & 0xFFu) | 0x20u;
+    const bool letter = (b0 == '-' || b0 == '+') && (b1 == 'i' || b1 == 'n');
+    bool ok;
+    const float f = fast::wfloat32m(w, nondigit16(w), *dt, &ok);
+    if (ok && !letter) return f;
+  }
+  uint64_t e;
+  return parse_float(src, x, &e, nan_err);
+}
 
 struct Seg {
   uint64_t lo, hi;      // [lo, hi) absolute
@@ -126,7 +187,8 @@ DA_HD bool r1_bit(const uint32_t *bits, uint64_t w0, uint64_t x) {
 // and emit (decode + store at base + local rank).
 template <int MODE>
 DA_HDF void walk(const LibsvmArgs &a, Src &src, const uint32_t *r1bits, uint64_t w0, const Seg &sg,
-                 uint32_t &st, Cnt &cnt, const Base64 &base, MinAcc *macc = nullptr) {
+                 uint32_t &st, Cnt &cnt, const Base64 &base, MinAcc *macc = nullptr,
+                 const fast::DecTables *dt = nullptr) {
   uint32_t ev = sg.rs | sg.ls | sg.le;
   int chunk = sg.chunk;
   uint64_t cfloor = a.cs[chunk], cend = a.cs[chunk + 1];
@@ -215,7 +277,7 @@ DA_HDF void walk(const LibsvmArgs &a, Src &src, const uint32_t *r1bits, uint64_t
         if (role == 1) {
           if (MODE == 2 || macc) {
             uint64_t v;
-            if (!parse_uint(src, x, a.wide != 0, &v)) {
+            if (!index_at(src, x, a.wide != 0, dt, &v)) {
               raise_error(a.err, E_NEG_INDEX, x);
               v = 0;
             }
@@ -237,8 +299,11 @@ DA_HDF void walk(const LibsvmArgs &a, Src &src, const uint32_t *r1bits, uint64_t
           if (MODE == 2) {
             const uint64_t vr = base.c[C_VALUE] + cnt.c[C_VALUE];
             bool nan_err = false;
-            uint64_t e;
-            const float v = parse_float(src, x, &e, &nan_err);
+#ifdef FSVM_ABL_EXNODEC  // timing ablation only (tools/build_variants.sh), never shipped
+            const float v = (float)(x & 7u);
+#else
+            const float v = value_at(src, x, dt, &nan_err);
+#endif
             if (nan_err) raise_error(a.err, E_NAN_LITERAL, x);
             if (vr < a.cap[C_VALUE]) a.value[vr] = v;
             else raise_error(a.err, E_CAPACITY, x);
@@ -309,6 +374,12 @@ DA_HDF void tile(const LibsvmArgs &a, Shared &sh, BK &bk, uint64_t k) {
     return;
   }
   if (tid == 0) sh.pending[1] = kNone;
+  fast::init_dec_tables(sh.dt, bk);
+#ifdef FSVM_EXACT_BYTEDEC  // A/B only: the byte decoders everywhere
+  const fast::DecTables *dtp = nullptr;
+#else
+  const fast::DecTables *dtp = &sh.dt;
+#endif
   bk.sync();
   int j = 0;             // window counter
   uint32_t st0 = S_PRE;  // concrete role state at the window start
@@ -415,7 +486,7 @@ DA_HDF void tile(const LibsvmArgs &a, Shared &sh, BK &bk, uint64_t k) {
     Cnt c = zero;
     if (sg.lo < sg.hi) {
       uint32_t s2 = st;
-      walk<1>(a, src, sh.r1bits, w0, sg, s2, c, nob, mp);
+      walk<1>(a, src, sh.r1bits, w0, sg, s2, c, nob, mp, dtp);
     }
     if (MODE == 1) {
       mine = CntAdd()(mine, c);
@@ -427,7 +498,7 @@ DA_HDF void tile(const LibsvmArgs &a, Shared &sh, BK &bk, uint64_t k) {
         for (int i = 0; i < C_N; ++i) b.c[i] = tbase.c[i] + tot.c[i] + ex.c[i];
         Cnt local = zero;
         uint32_t s3 = st;
-        walk<2>(a, src, sh.r1bits, w0, sg, s3, local, b);
+        walk<2>(a, src, sh.r1bits, w0, sg, s3, local, b, nullptr, dtp);
       }
       tot = CntAdd()(tot, wtot);
     }

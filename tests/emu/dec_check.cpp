@@ -8,6 +8,7 @@
 #include <string>
 
 #include "fast_common.h"
+#include "libsvm_core.h"
 
 using namespace dmlc_amd;
 using namespace dmlc_amd::fast;
@@ -83,6 +84,52 @@ int main(int argc, char **argv) {
       }
     }
   }
-  printf("strings %ld, float fast %ld, uint fast %ld, mismatches %ld\n", n, fast_f, fast_i, bad);
+  // the exact kernels' use (libsvm_core.h value_at / index_at): a run that
+  // starts with a digitchar, followed by any bytes (letters, inf / nan,
+  // bytes >= 0x80); the window result must equal the byte decoder's
+  long ex_f = 0;
+  for (long it = 0; it < n; ++it) {
+    std::string s;
+    const char *head = "0123456789+-.eE";
+    s += head[rnd() % strlen(head)];
+    const char *al = "0123456789012345678901234567890123456789..eE+-infaINFANx :#\t";
+    const int m = (int)(rnd() % 24);
+    for (int i = 0; i < m; ++i) {
+      const uint64_t r = rnd() % 64;
+      if (r == 0) s += (char)(0x80 + rnd() % 128);
+      else if (r == 1) s += "inf";
+      else if (r == 2) s += "nan";
+      else s += al[rnd() % strlen(al)];
+    }
+    while (s.size() < 48) s += (char)(rnd() % 2 ? ' ' : '\n');
+    const uint8_t *p = reinterpret_cast<const uint8_t *>(s.data());
+    const uint64_t lim = 16 + rnd() % 24;  // the chunk end: bytes at or past it read as NUL
+    Src src;
+    src.g = p;
+    src.lim = lim;
+    src.lds = p;
+    src.wbase = 0;
+    src.wend = s.size();
+    GSrc at{p, lim};
+    bool ne1 = false, ne2 = false;
+    uint64_t e;
+    const float v = svm::value_at(src, 0, &tb, &ne1);
+    const float r = parse_float(at, 0, &e, &ne2);
+    ++ex_f;
+    if (memcmp(&v, &r, 4) || ne1 != ne2) {
+      if (bad++ < 10) printf("exact float mismatch '%.24s' win=%.9g byte=%.9g\n", s.c_str(), v, r);
+    }
+    for (int wide = 0; wide < 2; ++wide) {
+      uint64_t a = 0, b = 0;
+      const bool pa = svm::index_at(src, 0, wide, &tb, &a);
+      const bool pb = parse_uint(at, 0, wide, &b);
+      if (pa != pb || (pa && a != b)) {
+        if (bad++ < 10) printf("exact uint mismatch '%.24s' win=%llu byte=%llu\n", s.c_str(),
+                               (unsigned long long)a, (unsigned long long)b);
+      }
+    }
+  }
+  printf("strings %ld, float fast %ld, uint fast %ld, exact-form %ld, mismatches %ld\n", n, fast_f, fast_i,
+         ex_f, bad);
   return bad != 0;
 }

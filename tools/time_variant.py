@@ -18,13 +18,15 @@ fmt, rows, width, kind = {"libsvm": ("libsvm", 1 << 20, 128, synth.LIBSVM), "csv
                           "qid": ("libsvm", 1 << 20, 128, synth.LIBSVM_QID),
                           "cmt": ("libsvm", 1 << 20, 128, synth.LIBSVM_CMT),
                           "libfm": ("libfm", 1 << 20, 64, synth.LIBFM),
-                          "csv_nan": ("csv", 1 << 20, 256, synth.CSV_NAN)}[cfg]
+                          "csv_nan": ("csv", 1 << 20, 256, synth.CSV_NAN),
+                          "exact": ("libsvm", 1 << 20, 128, synth.LIBSVM),
+                          "csv_exact": ("csv", 1 << 20, 256, synth.CSV)}[cfg]
 text, _ = synth.rows(kind, rows, width, seed=1)
 starts = dmlc_amd.text_chunk_starts(text)
 dev = torch.device("cuda", 0)
 d_text = torch.from_numpy(text).to(dev)
 d_starts = torch.from_numpy(starts).to(dev)
-p = dmlc_amd.DeviceParser(fmt)
+p = dmlc_amd.DeviceParser(fmt, flags=dmlc_amd.FLAG_EXACT if cfg.endswith("exact") else 0)
 res = torch.zeros(16, dtype=torch.int64, device=dev)
 counts = p.count(d_text, d_starts, result=res)
 out = p.alloc(counts)
