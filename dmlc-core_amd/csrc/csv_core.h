@@ -16,6 +16,7 @@
 #pragma once
 #include "args.h"
 #include "decode.h"
+#include "exact_dec.h"
 
 namespace dmlc_amd {
 namespace csv {
@@ -62,11 +63,12 @@ struct Field {
   bool nan_err;
 };
 
-DA_HD Field decode_field(const Src &at, int vtype, uint64_t p) {
+DA_HD Field decode_field(const Src &at, int vtype, uint64_t p, const fast::DecTables *dt = nullptr) {
   Field r;
   r.nan_err = false;
   r.f = 0.f;
   r.i = 0;
+  if (vtype == 0 && csv_value_at(at, p, dt, &r.f, &r.end)) return r;  // in registers (exact_dec.h)
   if (vtype == 0) {
     r.f = parse_float(at, p, &r.end, &r.nan_err);
   } else {
@@ -172,7 +174,7 @@ DA_HD bool is_value_col(const CsvArgs &a, uint64_t c) {
 
 template <int MODE>  // 1 count, 2 emit
 DA_HDF void walk(const CsvArgs &a, Src &src, const Seg &sg, uint32_t state, Cnt &cnt,
-                     const Base64 &base) {
+                     const Base64 &base, const fast::DecTables *dt) {
   uint32_t ev = sg.ls | sg.dl | sg.fs;
   int chunk = sg.chunk;
   uint64_t cend = a.cs[chunk + 1];
@@ -218,7 +220,7 @@ DA_HDF void walk(const CsvArgs &a, Src &src, const Seg &sg, uint32_t state, Cnt 
     }
     if (!in_line || slow) continue;
     if ((sg.fs >> i) & 1u) {
-      Field f = decode_field(src, a.vtype, x);
+      Field f = decode_field(src, a.vtype, x, dt);
       if (MODE == 2 && f.nan_err) raise_error(a.err, E_NAN_LITERAL, x);
       const bool vc = is_value_col(a, col);
       if ((int64_t)col == a.label_column) {
@@ -293,6 +295,7 @@ DA_HDF uint64_t first_line_start(const CsvArgs &a, BK &bk, uint64_t from, uint64
 
 struct Shared {
   uint8_t win[kWin + 32];
+  fast::DecTables dt;  // the window decoders' tables (exact_dec.h)
 };
 
 // The tile body.  MODE 1 = count pass, MODE 2 = write pass.
@@ -318,6 +321,12 @@ DA_HDF void tile(const CsvArgs &a, Shared &sh, BK &bk, uint64_t k) {
   Src src;
   src.g = a.text;
   src.lds = sh.win;
+  fast::init_dec_tables(sh.dt, bk);  // (read after the window's barrier)
+#ifdef FSVM_EXACT_BYTEDEC  // A/B only: the byte decoders everywhere
+  const fast::DecTables *dtp = nullptr;
+#else
+  const fast::DecTables *dtp = &sh.dt;
+#endif
   while (!done) {
     uint64_t wend = mn(w0 + (uint64_t)kWin, a.n);
     if (wend == a.n) done = true;
@@ -403,7 +412,7 @@ DA_HDF void tile(const CsvArgs &a, Shared &sh, BK &bk, uint64_t k) {
     Base64 nob;
     for (int i = 0; i < C_N; ++i) nob.c[i] = 0;
     Cnt cc = zero;
-    if (sg.lo < sg.hi) walk<1>(a, src, sg, in_state, cc, nob);
+    if (sg.lo < sg.hi) walk<1>(a, src, sg, in_state, cc, nob, dtp);
     if (MODE == 1) {
       mine = CntAdd()(mine, cc);
     } else {
@@ -413,7 +422,7 @@ DA_HDF void tile(const CsvArgs &a, Shared &sh, BK &bk, uint64_t k) {
         Base64 b;
         for (int i = 0; i < C_N; ++i) b.c[i] = tbase.c[i] + tot.c[i] + ex.c[i];
         Cnt local = zero;
-        walk<2>(a, src, sg, in_state, local, b);
+        walk<2>(a, src, sg, in_state, local, b, dtp);
       }
       tot = CntAdd()(tot, wtot);
     }

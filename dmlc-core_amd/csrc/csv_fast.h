@@ -88,13 +88,14 @@ DA_HD uint32_t infinity_len(uint64_t lo) {  // lo: the 8 bytes at p, little-endi
   return x ? (uint32_t)ctz64(x) >> 3 : 8u;
 }
 // the bytes at p start ParseFloat's "inf" / "infinity" or "nan":
-// 1 inf, 2 nan, 3 "nan(" (its NAN(chars) form), 0 neither
-DA_HD uint32_t csv_inf_nan(const uint8_t *p) {
+// 1 inf, 2 nan, 3 "nan(" (its NAN(chars) form), 0 neither.  nv: the bytes
+// before the InputSplit chunk end (ParseFloat reads NUL from there on).
+DA_HD uint32_t csv_inf_nan(const uint8_t *p, uint64_t nv) {
   uint64_t lo = 0;
-  for (int i = 0; i < 8; ++i) lo |= (uint64_t)p[i] << (8 * i);
+  for (int i = 0; i < 8; ++i) lo |= (uint64_t)((uint64_t)i < nv ? p[i] : 0u) << (8 * i);
   const uint32_t k = infinity_len(lo);
   if (k == 3u || k == 8u) return 1u;
-  if (((lo | 0x202020u) & 0xFFFFFFu) == 0x6E616Eu) return p[3] == '(' ? 3u : 2u;
+  if (((lo | 0x202020u) & 0xFFFFFFu) == 0x6E616Eu) return nv > 3u && p[3] == '(' ? 3u : 2u;
   return 0u;
 }
 // ParseFloat's INF / NAN branch (strtonum.h:133-175) on a token window whose
@@ -461,19 +462,20 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
           // inf_nan_of; also after a sign: "-inf" is a number-char token);
           // "nan(" goes to the exact kernels
           const uint8_t *seg = sh.c.text + kPre + tid * kSegB;
+          auto nv = [&](uint64_t i) { return t.next_cs(P + i) - (P + i); };  // bytes to the chunk end
           for (uint64_t m = F & J; m; m &= m - 1) {
-            const uint32_t i = (uint32_t)ctz64(m), k = csv_inf_nan(seg + i);
+            const uint32_t i = (uint32_t)ctz64(m), k = csv_inf_nan(seg + i, nv(i));
             if (k == 3u) bad = 1;
             else if (k != 0u || (seg[i] | 0x20u) == 'f') T |= m & (0 - m);
           }
           for (uint64_t m = land & J; m; m &= m - 1)
-            if (csv_inf_nan(seg + ctz64(m)) == 3u) bad = 1;
+            if (csv_inf_nan(seg + ctz64(m), nv(ctz64(m))) == 3u) bad = 1;
           const uint64_t FD = F & D;
           uint64_t Jn = J >> 1;  // junk after the byte (a sign's next byte)
           if (FD >> 63) Jn |= (uint64_t)csv_junk_byte(seg[kSegB]) << 63;
           for (uint64_t m = FD & Jn; m; m &= m - 1) {
             const uint32_t i = (uint32_t)ctz64(m), b = seg[i];
-            if ((b == '-' || b == '+') && csv_inf_nan(seg + i + 1) == 3u) bad = 1;
+            if ((b == '-' || b == '+') && csv_inf_nan(seg + i + 1, nv(i + 1)) == 3u) bad = 1;
           }
         }
       } else {

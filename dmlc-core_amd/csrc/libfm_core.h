@@ -87,7 +87,8 @@ DA_HD uint64_t prev_run(const F &at, uint64_t x, uint64_t floor) {
 // st; MODE 1: count from concrete state st; MODE 2: count and emit.
 template <int MODE>
 DA_HDF void walk(const LibfmArgs &a, Src &src, const uint32_t *r1bits, uint64_t w0, const Seg &sg,
-                 uint32_t &st, Cnt &cnt, const Base64 &base, MinAcc *macc = nullptr) {
+                 uint32_t &st, Cnt &cnt, const Base64 &base, MinAcc *macc = nullptr,
+                 const fast::DecTables *dt = nullptr) {
   uint32_t ev = sg.rs | sg.ls | sg.le;
   int chunk = sg.chunk;
   uint64_t cfloor = a.cs[chunk], cend = a.cs[chunk + 1];
@@ -96,8 +97,8 @@ DA_HDF void walk(const LibfmArgs &a, Src &src, const uint32_t *r1bits, uint64_t 
   auto pair = [&](uint64_t fpos, uint64_t ipos, uint64_t x) {
     if (MODE == 2 || macc) {
       uint64_t fv, iv;
-      bool ok = parse_uint(src, fpos, a.wide != 0, &fv);
-      ok = parse_uint(src, ipos, a.wide != 0, &iv) && ok;
+      bool ok = index_at(src, fpos, a.wide != 0, dt, &fv);  // (exact_dec.h)
+      ok = index_at(src, ipos, a.wide != 0, dt, &iv) && ok;
       if (!ok) {
         raise_error(a.err, E_NEG_INDEX, x);
         fv = iv = 0;
@@ -134,8 +135,7 @@ DA_HDF void walk(const LibfmArgs &a, Src &src, const uint32_t *r1bits, uint64_t 
     if (MODE == 2) {
       const uint64_t r = base.c[C_VALUE] + cnt.c[C_VALUE];
       bool nan_err = false;
-      uint64_t e;
-      const float v = parse_float(src, vpos, &e, &nan_err);
+      const float v = value_at(src, vpos, dt, &nan_err);
       if (nan_err) raise_error(a.err, E_NAN_LITERAL, x);
       if (r < a.cap[C_VALUE]) a.value[r] = v;
       else raise_error(a.err, E_CAPACITY, x);
@@ -204,10 +204,8 @@ DA_HDF void walk(const LibfmArgs &a, Src &src, const uint32_t *r1bits, uint64_t 
         }
         if (role != S_PRE) st = role;
         if (role == S_A) {  // v1 of a triple: the reference decodes it even if dropped
-          if (MODE == 2) {
-            uint64_t v;
-            if (!parse_uint(src, x, a.wide != 0, &v)) raise_error(a.err, E_NEG_INDEX, x);
-          }
+          // (ParseUnsignedInt fails only on a leading '-': x starts a digitchar run)
+          if (MODE == 2 && src(x) == '-') raise_error(a.err, E_NEG_INDEX, x);
         } else if (role == S_B) {
           pair(prev_run(src, x, cfloor), x, x);
         } else if (role == S_C) {
@@ -245,6 +243,12 @@ DA_HDF void tile(const LibfmArgs &a, svm::Shared &sh, BK &bk, uint64_t k) {
     return;
   }
   if (tid == 0) sh.pending[1] = kNone;
+  fast::init_dec_tables(sh.dt, bk);
+#ifdef FSVM_EXACT_BYTEDEC  // A/B only: the byte decoders everywhere
+  const fast::DecTables *dtp = nullptr;
+#else
+  const fast::DecTables *dtp = &sh.dt;
+#endif
   bk.sync();
   int j = 0;             // window counter
   uint32_t st0 = S_PRE;  // concrete state at the window start
@@ -348,7 +352,7 @@ DA_HDF void tile(const LibfmArgs &a, svm::Shared &sh, BK &bk, uint64_t k) {
     Cnt c = zero;
     if (sg.lo < sg.hi) {
       uint32_t s2 = st;
-      walk<1>(a, src, sh.r1bits, w0, sg, s2, c, nob, mp);
+      walk<1>(a, src, sh.r1bits, w0, sg, s2, c, nob, mp, dtp);
     }
     if (MODE == 1) {
       mine = CntAdd()(mine, c);
@@ -360,7 +364,7 @@ DA_HDF void tile(const LibfmArgs &a, svm::Shared &sh, BK &bk, uint64_t k) {
         for (int i = 0; i < C_N; ++i) b.c[i] = tbase.c[i] + tot.c[i] + ex.c[i];
         Cnt local = zero;
         uint32_t s3 = st;
-        walk<2>(a, src, sh.r1bits, w0, sg, s3, local, b);
+        walk<2>(a, src, sh.r1bits, w0, sg, s3, local, b, nullptr, dtp);
       }
       tot = CntAdd()(tot, wtot);
     }

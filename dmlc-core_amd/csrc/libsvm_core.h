@@ -19,7 +19,7 @@
 #pragma once
 #include "args.h"
 #include "decode.h"
-#include "fast_common.h"
+#include "exact_dec.h"
 
 namespace dmlc_amd {
 namespace svm {
@@ -112,64 +112,6 @@ struct Shared {  // LDS of one workgroup
   fast::DecTables dt;   // the window decoders' tables (fast_common.h)
 };
 
-// The 16 bytes at x from the staged window (two aligned LDS words per output
-// word, funnel-shifted), when all of them lie inside the window and before
-// the chunk end: the run at x can then be decoded in registers by the
-// window decoders of the single-pass kernels (fast_common.h wfloat32 /
-// wuint32), which report when the run does not fit their form -- the byte
-// decoders of decode.h take those.
-DA_HD bool win16(const Src &s, uint64_t x, uint32_t w[4]) {
-  if (x < s.wbase || x + 16 > s.wend || x + 16 > s.lim) return false;
-  const uint64_t o = x - s.wbase;
-  const uint32_t *q = reinterpret_cast<const uint32_t *>(s.lds + (o & ~3ull));
-  const uint32_t sh = 8u * (uint32_t)(o & 3u);
-  uint32_t v[5];
-  for (int i = 0; i < 5; ++i) v[i] = q[i];
-  for (int i = 0; i < 4; ++i) w[i] = fast::funnel(v[i + 1], v[i], sh);
-  return true;
-}
-// bit i: window byte i is not '0'..'9' -- any byte value (fast_common.h nd4
-// assumes bytes < 0x80, which the single-pass grammar guarantees and the
-// text of the exact kernels does not)
-DA_HD uint32_t nondigit16(const uint32_t w[4]) {
-  uint32_t m = 0;
-  for (int i = 0; i < 4; ++i) {
-    const uint32_t y = w[i] & 0x7F7F7F7Fu;
-    const uint32_t t = ((((y ^ 0x30303030u) + 0x76767676u) | w[i]) >> 7) & 0x01010101u;
-    m |= fast::udot4(t, 0x08040201u, 0u) << (4 * i);
-  }
-  return m;
-}
-// ParseUnsignedInt of the run at x through the window when it fits (a '-' or
-// more than 8 digits: the byte decoder, which also raises the '-' error)
-DA_HD bool index_at(const Src &src, uint64_t x, bool wide, const fast::DecTables *dt, uint64_t *v) {
-  uint32_t w[4];
-  if (dt && win16(src, x, w)) {
-    bool ok;
-    uint64_t t;
-    const bool pos = fast::wuint32m(w, nondigit16(w), *dt, &t, &ok);
-    if (ok && pos) {
-      *v = t;
-      return true;
-    }
-  }
-  return parse_uint(src, x, wide, v);
-}
-// ParseFloat<float> of the run at x through the window when it fits.  Beyond
-// the single-pass grammar, a sign followed by inf / nan letters is left to
-// the byte decoder (wfloat32 reads it as a signed zero).
-DA_HD float value_at(const Src &src, uint64_t x, const fast::DecTables *dt, bool *nan_err) {
-  uint32_t w[4];
-  if (dt && win16(src, x, w)) {
-    const uint32_t b0 = w[0] & 0xFFu, b1 = ((w[0] >> 8) & 0xFFu) | 0x20u;
-    const bool letter = (b0 == '-' || b0 == '+') && (b1 == 'i' || b1 == 'n');
-    bool ok;
-    const float f = fast::wfloat32m(w, nondigit16(w), *dt, &ok);
-    if (ok && !letter) return f;
-  }
-  uint64_t e;
-  return parse_float(src, x, &e, nan_err);
-}
 
 struct Seg {
   uint64_t lo, hi;      // [lo, hi) absolute

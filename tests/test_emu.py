@@ -577,7 +577,11 @@ def test_emu_csv_chunk_cut_edges(vt):
     borrow the next chunk's bytes."""
     cases = [(b"1,-5,2\n", [0, 3, 7]), (b"1,+7\n4\n", [0, 3, 8]), (b"1,  \n 2,3\n", [0, 3, 11]),
              (b"1, 2,3\n", [0, 3, 7]), (b"5, ,  6\n", [0, 4, 8]), (b"-\n9,1\n", [0, 1, 6]),
-             (b"1|  |2\n", [0, 3, 7]), (b" 7, 8\n 9\n", [0, 1, 10])]
+             (b"1|  |2\n", [0, 3, 7]), (b" 7, 8\n 9\n", [0, 1, 10]),
+             # inf / nan tokens cut by the chunk end: the letters after it are
+             # the next chunk's (ParseFloat reads NUL there)
+             (b"1,inf\n2,3\n", [0, 3, 10]), (b"1,nan(2)\n2\n", [0, 5, 11]), (b"1,-inf\n2\n", [0, 4, 9]),
+             (b"x,1\ni\rinfo,9\n", [0, 6, 14]), (b"1,infinity\n", [0, 8, 11])]
     for data, offs in cases:
         kw = {"value_type": vt}
         okw = {"value_kind": vt}

@@ -20,7 +20,8 @@ fmt, rows, width, kind = {"libsvm": ("libsvm", 1 << 20, 128, synth.LIBSVM), "csv
                           "libfm": ("libfm", 1 << 20, 64, synth.LIBFM),
                           "csv_nan": ("csv", 1 << 20, 256, synth.CSV_NAN),
                           "exact": ("libsvm", 1 << 20, 128, synth.LIBSVM),
-                          "csv_exact": ("csv", 1 << 20, 256, synth.CSV)}[cfg]
+                          "csv_exact": ("csv", 1 << 20, 256, synth.CSV),
+                          "libfm_exact": ("libfm", 1 << 20, 64, synth.LIBFM)}[cfg]
 text, _ = synth.rows(kind, rows, width, seed=1)
 starts = dmlc_amd.text_chunk_starts(text)
 dev = torch.device("cuda", 0)
