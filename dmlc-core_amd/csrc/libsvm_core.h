@@ -395,7 +395,11 @@ DA_HDF void tile(const LibsvmArgs &a, Shared &sh, BK &bk, uint64_t k) {
     }
 
     // ---- head sections -> R1 marks
+#ifdef FSVM_ABL_EX_NOHEAD  // timing ablation only
+    if (false) {
+#else
     if (sg.ls) {
+#endif
       uint32_t m = sg.ls;
       int chunk = sg.chunk;
       while (m) {
@@ -418,7 +422,9 @@ DA_HDF void tile(const LibsvmArgs &a, Shared &sh, BK &bk, uint64_t k) {
     Cnt dummy = zero;
     Base64 nob;
     for (int i = 0; i < C_N; ++i) nob.c[i] = 0;
+#ifndef FSVM_ABL_EX_NOW0  // timing ablation only (tools/build_variants.sh), never shipped
     if (sg.lo < sg.hi) walk<0>(a, src, sh.r1bits, w0, sg, fn, dummy, nob);
+#endif
     uint32_t fn_total;
     const uint32_t fn_ex = bk.exclusive(fn, kIdentityFn, FnCompose(), &fn_total);
     const uint32_t st = (fn_ex >> (2 * st0)) & 3u;
@@ -428,6 +434,11 @@ DA_HDF void tile(const LibsvmArgs &a, Shared &sh, BK &bk, uint64_t k) {
     Cnt c = zero;
     if (sg.lo < sg.hi) {
       uint32_t s2 = st;
+#ifndef FSVM_ABL_EX_NOW1  // timing ablation only
+      if (MODE == 1 || true)
+#else
+      if (MODE == 1)
+#endif
       walk<1>(a, src, sh.r1bits, w0, sg, s2, c, nob, mp, dtp);
     }
     if (MODE == 1) {
@@ -440,7 +451,9 @@ DA_HDF void tile(const LibsvmArgs &a, Shared &sh, BK &bk, uint64_t k) {
         for (int i = 0; i < C_N; ++i) b.c[i] = tbase.c[i] + tot.c[i] + ex.c[i];
         Cnt local = zero;
         uint32_t s3 = st;
+#ifndef FSVM_ABL_EX_NOW2  // timing ablation only
         walk<2>(a, src, sh.r1bits, w0, sg, s3, local, b, nullptr, dtp);
+#endif
       }
       tot = CntAdd()(tot, wtot);
     }

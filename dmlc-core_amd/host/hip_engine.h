@@ -691,7 +691,8 @@ class HipTextParser : public dmlc::Parser<IndexType, DType> {
         pre_dst[5] = b->field.reserve(w->est[5] / isz + 1);
         pre_dst[6] = b->value.reserve(w->est[6] / dsz + 1);
         pre_dst[7] = b->tab.reserve(nunits * 8);
-        for (int i = 0; i < 8; ++i) pre_max[i] = i == 7 ? (uint64_t)nunits * 64 : w->est[i];
+        // (an output the format does not have -- a NULL array -- is not copied)
+        for (int i = 0; i < 8; ++i) pre_max[i] = !src[i] ? 0 : i == 7 ? (uint64_t)nunits * 64 : w->est[i];
         CheckRc(dmlc_amd_copy_n_dev(pre_dst, src, d_res, kSlot, kScale, kAdd, pre_max, 8, s));
       }
       hip_check(hipMemcpyAsync(hres, d_res, sizeof(dmlc_amd_result), hipMemcpyDeviceToHost, s), "D2H result");
@@ -726,7 +727,7 @@ class HipTextParser : public dmlc::Parser<IndexType, DType> {
     bool again = !pre;
     for (int i = 0; i < 8; ++i) {
       again = again || nb[i] > pre_max[i] || (nb[i] && dst[i] != pre_dst[i]);
-      w->est[i] = std::max<uint64_t>(w->est[i], (nb[i] + nb[i] / 4 + 4095) & ~uint64_t(15));
+      if (nb[i]) w->est[i] = std::max<uint64_t>(w->est[i], (nb[i] + nb[i] / 4 + 4095) & ~uint64_t(15));
     }
     if (again) {
       if (cfg_.d2h_kernel()) CheckRc(dmlc_amd_copy_n(dst, src, nb, 8, s));

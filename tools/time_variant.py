@@ -27,7 +27,8 @@ starts = dmlc_amd.text_chunk_starts(text)
 dev = torch.device("cuda", 0)
 d_text = torch.from_numpy(text).to(dev)
 d_starts = torch.from_numpy(starts).to(dev)
-p = dmlc_amd.DeviceParser(fmt, flags=dmlc_amd.FLAG_EXACT if cfg.endswith("exact") else 0)
+p = dmlc_amd.DeviceParser(fmt, flags=dmlc_amd.FLAG_EXACT if cfg.endswith("exact") else 0,
+                          tile_bytes=int(os.environ.get("TILE_BYTES", "0")))
 res = torch.zeros(16, dtype=torch.int64, device=dev)
 counts = p.count(d_text, d_starts, result=res)
 out = p.alloc(counts)
@@ -36,10 +37,13 @@ for _ in range(3):
     p.parse_into(d_text, d_starts, out, res)
 torch.cuda.synchronize()
 dmlc_amd.profile_begin()
+t0 = time.perf_counter()
 for _ in range(10):
     p.parse_into(d_text, d_starts, out, res)
 torch.cuda.synchronize()
+call_ms = (time.perf_counter() - t0) * 100.0  # per call, whole pipeline
 ms, n, name = dmlc_amd.profile_end()
 r = res.cpu().numpy().view(np.uint64)
-print("%s %s %.4f ms path=%d err=%#x res15=%d" % (os.path.basename(os.environ.get("DMLC_AMD_LIB", "default")),
-                                                  name, ms / max(n, 1), int(r[9]), int(r[8]), int(r[15])))
+print("tile=%s %s %s %.4f ms call %.3f ms path=%d err=%#x res15=%d" % (os.environ.get("TILE_BYTES", "0"),
+                                                          os.path.basename(os.environ.get("DMLC_AMD_LIB", "default")),
+                                                  name, ms / max(n, 1), call_ms, int(r[9]), int(r[8]), int(r[15])))
