@@ -124,13 +124,28 @@ DA_HD bool r1_bit(const uint32_t *bits, uint64_t w0, uint64_t x) {
   return (bits[o >> 5] >> (o & 31)) & 1u;
 }
 
-// Event walk over one segment.  MODE 0: compose the role-machine transition
-// function into st; MODE 1: count roles from concrete state st; MODE 2: count
-// and emit (decode + store at base + local rank).
-template <int MODE>
-DA_HDF void walk(const LibsvmArgs &a, Src &src, const uint32_t *r1bits, uint64_t w0, const Seg &sg,
-                 uint32_t &st, Cnt &cnt, const Base64 &base, MinAcc *macc = nullptr,
-                 const fast::DecTables *dt = nullptr) {
+// Role masks of one segment for each role-machine state at its start: bit i
+// of idx[s] / val[s] = the run starting at lo + i is an index / a value when
+// the segment starts in state s; dng[s] = a dangling "idx:" at the line end
+// at lo + i, whose value ParsePair decodes at lo + i + 1.  The block scan of
+// the transition functions then picks one set, and the counts are popcounts.
+struct Roles {
+  uint32_t idx[4], val[4], dng[4];
+};
+DA_HD uint32_t pick(const uint32_t m[4], uint32_t s) {  // m[s] without a dynamic register index
+  return s == 0 ? m[0] : s == 1 ? m[1] : s == 2 ? m[2] : m[3];
+}
+
+// Event walk over one segment: compose the role machine's transition
+// function into fn (4 x 2-bit entries, entry s = the state after the events
+// when the segment starts in s) and record the role masks.  ParsePair
+// (strtonum.h:667-703) for libsvm_parser.h:134-161: a run is an index after
+// the line head (R1) or a previous pair, a value when ':' is the first
+// non-blank of the gap after an index; '#' as that first non-blank drops the
+// rest of the line (IgnoreCommentAndBlank, :67-83).
+DA_HDF void walk_roles(const LibsvmArgs &a, Src &src, const uint32_t *r1bits, uint64_t w0, const Seg &sg,
+                       uint32_t &fn, Roles &R) {
+  for (int s = 0; s < 4; ++s) R.idx[s] = R.val[s] = R.dng[s] = 0;
   uint32_t ev = sg.rs | sg.ls | sg.le;
   int chunk = sg.chunk;
   uint64_t cfloor = a.cs[chunk], cend = a.cs[chunk + 1];
@@ -138,136 +153,156 @@ DA_HDF void walk(const LibsvmArgs &a, Src &src, const uint32_t *r1bits, uint64_t
   while (ev) {
     const int i = ctz32(ev);
     ev &= ev - 1;
+    const uint32_t bit = 1u << i;
     const uint64_t x = sg.lo + i;
     while (x >= cend) {  // entered the next chunk
       ++chunk;
       cfloor = a.cs[chunk];
       cend = a.cs[chunk + 1];
-      src.lim = a.lim(chunk);  // decoders read to the InputSplit chunk end
+      src.lim = a.lim(chunk);
     }
-    if ((sg.ls >> i) & 1u) {
-      if (MODE == 0) {
-        st = 0u;  // every entry -> PRE
-      } else {
-        st = S_PRE;
-        const bool l0 = x == cfloor;
-        const Head h = head_parse(src, x, l0, cend);
-        if (MODE == 2 && l0) {
-          uint64_t *row = a.chunk_tab + (uint64_t)chunk * 8;  // rows of 8 slots (dmlc_amd.h)
-          for (int k = 0; k < C_N; ++k) row[k] = base.c[k] + cnt.c[k];
+    if (sg.ls & bit) fn = 0u;  // every entry -> PRE
+    if (sg.rs & bit) {
+      if (r1_bit(r1bits, w0, x)) {
+        fn = 0x55u;  // every entry -> FIRST, the run an index
+        for (int s = 0; s < 4; ++s) R.idx[s] |= bit;
+      } else if ((fn ^ (fn >> 1)) & 0x55u) {  // some entry is F or S
+        const uint32_t g = gap_fnb(src, x, cfloor);
+        const uint32_t tF = g == '#' ? S_D : (g == ':' ? S_S : S_F);
+        const uint32_t tS = g == '#' ? S_D : S_F;
+        for (int s = 0; s < 4; ++s) {
+          const uint32_t e = (fn >> (2 * s)) & 3u;
+          if (e == S_F && tF == S_S) R.val[s] |= bit;
+          else if ((e == S_F || e == S_S) && g != '#') R.idx[s] |= bit;
         }
-        if (h.row) {
-          if (MODE == 2) {
-            const uint64_t r = base.c[C_ROWS] + cnt.c[C_ROWS];
-            bool nan_err = false;
-            uint64_t e;
-            if (r < a.cap[C_ROWS]) {
-              a.label[r] = parse_float(src, h.label, &e, &nan_err);
-              a.offset[r] = base.c[C_INDEX] + cnt.c[C_INDEX];
-            } else {
-              raise_error(a.err, E_CAPACITY, x);
-            }
-            if (h.w) {
-              const uint64_t wr = base.c[C_WEIGHT] + cnt.c[C_WEIGHT];
-              if (wr < a.cap[C_WEIGHT]) a.weight[wr] = parse_float(src, h.wpos, &e, &nan_err);
-              else raise_error(a.err, E_CAPACITY, x);
-            }
-            if (h.q) {
-              const uint64_t qr = base.c[C_QID] + cnt.c[C_QID];
-              if (qr < a.cap[C_QID]) a.qid[qr] = (uint64_t)c_strtoll(src, h.qpos, 10, &e);
-              else raise_error(a.err, E_CAPACITY, x);
-            }
-            if (nan_err) raise_error(a.err, E_NAN_LITERAL, x);
-          }
-          cnt.c[C_ROWS]++;
-          cnt.c[C_LABEL]++;
-          cnt.c[C_WEIGHT] += h.w;
-          cnt.c[C_QID] += h.q;
-        }
+        fn = fn_apply(fn, S_PRE | (tF << 2) | (tS << 4) | (S_D << 6));
       }
     }
-    if ((sg.rs >> i) & 1u) {
-      if (MODE == 0) {
-        if (r1_bit(r1bits, w0, x)) {
-          st = 0x55u;  // every entry -> FIRST
+    if (sg.le & bit) {  // "idx:" dangling at the line end: ParsePair decodes the value at lend
+      uint32_t fF = 0;
+      for (int s = 0; s < 4; ++s) fF |= (((fn >> (2 * s)) & 3u) == S_F ? 1u : 0u) << s;
+      if (fF && gap_fnb(src, x + 1, cfloor) == ':')
+        for (int s = 0; s < 4; ++s)
+          if ((fF >> s) & 1u) R.dng[s] |= bit;
+    }
+  }
+}
+
+// Count pass, indexing_mode < 0: the unit minimum of the segment's indices
+DA_HDF void index_min(const LibsvmArgs &a, Src &src, const Seg &sg, uint32_t I, MinAcc *macc,
+                      const fast::DecTables *dt) {
+  int chunk = sg.chunk;
+  uint64_t cend = a.cs[chunk + 1];
+  src.lim = a.lim(chunk);
+  while (I) {
+    const int i = ctz32(I);
+    I &= I - 1;
+    const uint64_t x = sg.lo + i;
+    while (x >= cend) {
+      ++chunk;
+      cend = a.cs[chunk + 1];
+      src.lim = a.lim(chunk);
+    }
+    uint64_t v;
+    if (!index_at(src, x, a.wide != 0, dt, &v)) {
+      raise_error(a.err, E_NEG_INDEX, x);
+      v = 0;
+    }
+    macc->add(a.chunk_min, chunk, a.wide ? v : (uint64_t)(uint32_t)v);
+  }
+}
+
+// Write pass: emit the segment's rows and entries in text order at base +
+// the running local counts (I / V / Dg: the role masks of its start state).
+DA_HDF void emit(const LibsvmArgs &a, Src &src, const Seg &sg, uint32_t I, uint32_t V, uint32_t Dg,
+                 const Base64 &base, const fast::DecTables *dt) {
+  Cnt cnt = cnt_zero();
+  uint32_t ev = sg.ls | I | V | Dg;
+  int chunk = sg.chunk;
+  uint64_t cfloor = a.cs[chunk], cend = a.cs[chunk + 1];
+  src.lim = a.lim(chunk);  // decoders read to the InputSplit chunk end
+  while (ev) {
+    const int i = ctz32(ev);
+    ev &= ev - 1;
+    const uint32_t bit = 1u << i;
+    const uint64_t x = sg.lo + i;
+    while (x >= cend) {  // entered the next chunk
+      ++chunk;
+      cfloor = a.cs[chunk];
+      cend = a.cs[chunk + 1];
+      src.lim = a.lim(chunk);
+    }
+    if (sg.ls & bit) {
+      const bool l0 = x == cfloor;
+      if (l0) {
+        uint64_t *row = a.chunk_tab + (uint64_t)chunk * 8;  // rows of 8 slots (dmlc_amd.h)
+        for (int k = 0; k < C_N; ++k) row[k] = base.c[k] + cnt.c[k];
+      }
+      const Head h = head_parse(src, x, l0, cend);
+      if (h.row) {
+        const uint64_t r = base.c[C_ROWS] + cnt.c[C_ROWS];
+        bool nan_err = false;
+        uint64_t e;
+        if (r < a.cap[C_ROWS]) {
+          a.label[r] = parse_float(src, h.label, &e, &nan_err);
+          a.offset[r] = base.c[C_INDEX] + cnt.c[C_INDEX];
         } else {
-          const uint32_t fs = (st ^ (st >> 1)) & 0x55u;  // some entry is F or S
-          if (fs) {
-            const uint32_t g = gap_fnb(src, x, cfloor);
-            const uint32_t tF = g == '#' ? S_D : (g == ':' ? S_S : S_F);
-            const uint32_t tS = g == '#' ? S_D : S_F;
-            st = fn_apply(st, S_PRE | (tF << 2) | (tS << 4) | (S_D << 6));
-          }
+          raise_error(a.err, E_CAPACITY, x);
         }
-      } else {
-        uint32_t role = 0;  // 0 none, 1 index, 2 value
-        if (r1_bit(r1bits, w0, x)) {
-          st = S_F;
-          role = 1;
-        } else if (st == S_F || st == S_S) {
-          const uint32_t g = gap_fnb(src, x, cfloor);
-          if (g == '#') {
-            st = S_D;
-          } else if (g == ':' && st == S_F) {
-            st = S_S;
-            role = 2;
-          } else {
-            st = S_F;
-            role = 1;
-          }
-        }
-        if (role == 1) {
-          if (MODE == 2 || macc) {
-            uint64_t v;
-            if (!index_at(src, x, a.wide != 0, dt, &v)) {
-              raise_error(a.err, E_NEG_INDEX, x);
-              v = 0;
-            }
-            if (MODE == 1) {
-              macc->add(a.chunk_min, chunk, a.wide ? v : (uint64_t)(uint32_t)v);
-            } else {
-              if (a.indexing_mode > 0 || (a.indexing_mode < 0 && a.chunk_min[chunk] > 0)) --v;
-              const uint64_t ir = base.c[C_INDEX] + cnt.c[C_INDEX];
-              if (ir < a.cap[C_INDEX]) {
-                if (a.wide) reinterpret_cast<uint64_t *>(a.index)[ir] = v;
-                else reinterpret_cast<uint32_t *>(a.index)[ir] = (uint32_t)v;
-              } else {
-                raise_error(a.err, E_CAPACITY, x);
-              }
-            }
-          }
-          cnt.c[C_INDEX]++;
-        } else if (role == 2) {
-          if (MODE == 2) {
-            const uint64_t vr = base.c[C_VALUE] + cnt.c[C_VALUE];
-            bool nan_err = false;
-#ifdef FSVM_ABL_EXNODEC  // timing ablation only (tools/build_variants.sh), never shipped
-            const float v = (float)(x & 7u);
-#else
-            const float v = value_at(src, x, dt, &nan_err);
-#endif
-            if (nan_err) raise_error(a.err, E_NAN_LITERAL, x);
-            if (vr < a.cap[C_VALUE]) a.value[vr] = v;
-            else raise_error(a.err, E_CAPACITY, x);
-          }
-          cnt.c[C_VALUE]++;
-        }
-      }
-    }
-    if (MODE != 0 && ((sg.le >> i) & 1u) && st == S_F) {
-      // "idx:" dangling at the line end: ParsePair decodes the value at lend
-      if (gap_fnb(src, x + 1, cfloor) == ':') {
-        if (MODE == 2) {
-          const uint64_t vr = base.c[C_VALUE] + cnt.c[C_VALUE];
-          bool nan_err = false;
-          uint64_t e;
-          const float v = parse_float(src, x + 1, &e, &nan_err);
-          if (nan_err) raise_error(a.err, E_NAN_LITERAL, x);
-          if (vr < a.cap[C_VALUE]) a.value[vr] = v;
+        if (h.w) {
+          const uint64_t wr = base.c[C_WEIGHT] + cnt.c[C_WEIGHT];
+          if (wr < a.cap[C_WEIGHT]) a.weight[wr] = parse_float(src, h.wpos, &e, &nan_err);
           else raise_error(a.err, E_CAPACITY, x);
         }
-        cnt.c[C_VALUE]++;
+        if (h.q) {
+          const uint64_t qr = base.c[C_QID] + cnt.c[C_QID];
+          if (qr < a.cap[C_QID]) a.qid[qr] = (uint64_t)c_strtoll(src, h.qpos, 10, &e);
+          else raise_error(a.err, E_CAPACITY, x);
+        }
+        if (nan_err) raise_error(a.err, E_NAN_LITERAL, x);
+        cnt.c[C_ROWS]++;
+        cnt.c[C_LABEL]++;
+        cnt.c[C_WEIGHT] += h.w;
+        cnt.c[C_QID] += h.q;
       }
+    }
+    if (I & bit) {
+      uint64_t v;
+      if (!index_at(src, x, a.wide != 0, dt, &v)) {
+        raise_error(a.err, E_NEG_INDEX, x);
+        v = 0;
+      }
+      if (a.indexing_mode > 0 || (a.indexing_mode < 0 && a.chunk_min[chunk] > 0)) --v;
+      const uint64_t ir = base.c[C_INDEX] + cnt.c[C_INDEX];
+      if (ir < a.cap[C_INDEX]) {
+        if (a.wide) reinterpret_cast<uint64_t *>(a.index)[ir] = v;
+        else reinterpret_cast<uint32_t *>(a.index)[ir] = (uint32_t)v;
+      } else {
+        raise_error(a.err, E_CAPACITY, x);
+      }
+      cnt.c[C_INDEX]++;
+    } else if (V & bit) {
+      const uint64_t vr = base.c[C_VALUE] + cnt.c[C_VALUE];
+      bool nan_err = false;
+#ifdef FSVM_ABL_EXNODEC  // timing ablation only (tools/build_variants.sh), never shipped
+      const float v = (float)(x & 7u);
+#else
+      const float v = value_at(src, x, dt, &nan_err);
+#endif
+      if (nan_err) raise_error(a.err, E_NAN_LITERAL, x);
+      if (vr < a.cap[C_VALUE]) a.value[vr] = v;
+      else raise_error(a.err, E_CAPACITY, x);
+      cnt.c[C_VALUE]++;
+    }
+    if (Dg & bit) {
+      const uint64_t vr = base.c[C_VALUE] + cnt.c[C_VALUE];
+      bool nan_err = false;
+      uint64_t e;
+      const float v = parse_float(src, x + 1, &e, &nan_err);
+      if (nan_err) raise_error(a.err, E_NAN_LITERAL, x);
+      if (vr < a.cap[C_VALUE]) a.value[vr] = v;
+      else raise_error(a.err, E_CAPACITY, x);
+      cnt.c[C_VALUE]++;
     }
   }
 }
@@ -394,12 +429,10 @@ DA_HDF void tile(const LibsvmArgs &a, Shared &sh, BK &bk, uint64_t k) {
       sg.le = (sg.ls >> 1) | ((uint32_t)nxt << (len - 1));
     }
 
-    // ---- head sections -> R1 marks
-#ifdef FSVM_ABL_EX_NOHEAD  // timing ablation only
-    if (false) {
-#else
+    // ---- head sections -> R1 marks, and the segment's row / weight / qid
+    // counts (libsvm_parser.h:99-132)
+    uint32_t hrow = 0, hw = 0, hq = 0;
     if (sg.ls) {
-#endif
       uint32_t m = sg.ls;
       int chunk = sg.chunk;
       while (m) {
@@ -413,35 +446,36 @@ DA_HDF void tile(const LibsvmArgs &a, Shared &sh, BK &bk, uint64_t k) {
           if (h.r1 < wend) atomic_or_u32(&sh.r1bits[(h.r1 - w0) >> 5], 1u << ((h.r1 - w0) & 31));
           else sh.pending[j & 1] = h.r1;  // only the window's last line can get here
         }
+        if (h.row) {
+          ++hrow;
+          hw += h.w;
+          hq += h.q;
+        }
       }
     }
     bk.sync();
 
-    // ---- role-machine transition function of my segment, then block scan
+    // ---- role masks and transition function of my segment, then block scan
     uint32_t fn = kIdentityFn;
-    Cnt dummy = zero;
-    Base64 nob;
-    for (int i = 0; i < C_N; ++i) nob.c[i] = 0;
-#ifndef FSVM_ABL_EX_NOW0  // timing ablation only (tools/build_variants.sh), never shipped
-    if (sg.lo < sg.hi) walk<0>(a, src, sh.r1bits, w0, sg, fn, dummy, nob);
-#endif
+    Roles R;
+    if (sg.lo < sg.hi) walk_roles(a, src, sh.r1bits, w0, sg, fn, R);
+    else
+      for (int s2 = 0; s2 < 4; ++s2) R.idx[s2] = R.val[s2] = R.dng[s2] = 0;
     uint32_t fn_total;
     const uint32_t fn_ex = bk.exclusive(fn, kIdentityFn, FnCompose(), &fn_total);
     const uint32_t st = (fn_ex >> (2 * st0)) & 3u;
     const uint32_t st_next = (fn_total >> (2 * st0)) & 3u;
+    const uint32_t I = pick(R.idx, st), V = pick(R.val, st), Dg = pick(R.dng, st);
 
-    // ---- count walk, then (write pass) scan + emit walk
+    // ---- counts by popcount, then (write pass) scan + emit
     Cnt c = zero;
-    if (sg.lo < sg.hi) {
-      uint32_t s2 = st;
-#ifndef FSVM_ABL_EX_NOW1  // timing ablation only
-      if (MODE == 1 || true)
-#else
-      if (MODE == 1)
-#endif
-      walk<1>(a, src, sh.r1bits, w0, sg, s2, c, nob, mp, dtp);
-    }
+    c.c[C_ROWS] = c.c[C_LABEL] = hrow;
+    c.c[C_WEIGHT] = hw;
+    c.c[C_QID] = hq;
+    c.c[C_INDEX] = (uint32_t)popc32(I);
+    c.c[C_VALUE] = (uint32_t)popc32(V) + (uint32_t)popc32(Dg);
     if (MODE == 1) {
+      if (mp && I) index_min(a, src, sg, I, mp, dtp);
       mine = CntAdd()(mine, c);
     } else {
       Cnt wtot;
@@ -449,11 +483,7 @@ DA_HDF void tile(const LibsvmArgs &a, Shared &sh, BK &bk, uint64_t k) {
       if (sg.lo < sg.hi) {
         Base64 b;
         for (int i = 0; i < C_N; ++i) b.c[i] = tbase.c[i] + tot.c[i] + ex.c[i];
-        Cnt local = zero;
-        uint32_t s3 = st;
-#ifndef FSVM_ABL_EX_NOW2  // timing ablation only
-        walk<2>(a, src, sh.r1bits, w0, sg, s3, local, b, nullptr, dtp);
-#endif
+        emit(a, src, sg, I, V, Dg, b, dtp);
       }
       tot = CntAdd()(tot, wtot);
     }

@@ -78,8 +78,9 @@ def lib():
             L.dmlc_amd_copy_n.restype = ctypes.c_int
             L.dmlc_amd_copy_n.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p),
                                           ctypes.POINTER(ctypes.c_uint64), ctypes.c_int, ctypes.c_void_p]
-        L.dmlc_amd_fast_geometry.restype = ctypes.c_int
-        L.dmlc_amd_fast_geometry.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]
+        if hasattr(L, "dmlc_amd_fast_geometry"):  # (A/B builds of older sources lack it)
+            L.dmlc_amd_fast_geometry.restype = ctypes.c_int
+            L.dmlc_amd_fast_geometry.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]
         L.dmlc_amd_profile_begin.restype = ctypes.c_int
         L.dmlc_amd_profile_end.restype = ctypes.c_int
         L.dmlc_amd_profile_end.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int),
