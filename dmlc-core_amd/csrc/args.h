@@ -42,7 +42,25 @@ struct LibsvmArgs {
   const uint32_t *gate;  // when set, the tile kernels run only if *gate != 0
   UnitLim ul;            // decoder limit per unit
   DA_HD uint64_t lim(int unit) const { return ul.lim(unit); }
+  // libsvm: what the count pass learnt per window for the write pass (NULL:
+  // the write pass works it out again): rec [ntiles][rec_win][4][kThreads]
+  // words -- index / value / dangling-value role masks and packed head
+  // counts per thread -- and rec_meta [ntiles][rec_win][2]: the R1 carried
+  // past the window and the role state after it
+  uint32_t *rec;
+  uint64_t *rec_meta;
+  uint32_t rec_win;  // windows per tile with a record (the rest: worked out again)
 };
+// windows per exact tile with a count-pass record, and the record bytes
+// (libsvm_core.h); the records are kept only while they stay within about
+// the text's size
+DA_HD uint32_t exact_rec_win(uint64_t tile_bytes, uint64_t win_bytes) {
+  return (uint32_t)(tile_bytes / win_bytes + 3);
+}
+DA_HD uint64_t exact_rec_bytes(uint64_t ntiles, uint32_t rec_win, int threads) {
+  return ntiles * rec_win * ((uint64_t)threads * 16 + 16);
+}
+DA_HD bool exact_rec_on(uint64_t nbytes, uint64_t rec_bytes) { return rec_bytes <= nbytes + (64ull << 20); }
 
 // libfm exact tile kernels (libfm_core.h): the libsvm block plus field ids.
 struct LibfmArgs : LibsvmArgs {

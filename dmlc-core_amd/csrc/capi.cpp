@@ -5,6 +5,7 @@
 #include <vector>
 
 #include "dmlc_amd.h"
+#include "common.h"
 #include "dmlc_amd_kernels.h"
 
 namespace {
@@ -135,6 +136,14 @@ const char *dmlc_amd_error_string(int code) {
 int units_per_chunk(const dmlc_amd_params *p) { return p && p->nthread > 1 ? p->nthread : 1; }
 constexpr int kMaxNthread = 1 << 12;
 
+// the exact libsvm kernels' count-pass records (args.h exact_rec_*): bytes,
+// 0 when the format has none or they would outgrow the text
+uint64_t rec_bytes_of(uint64_t nbytes, uint64_t T, uint64_t ntiles, const dmlc_amd_params *prm) {
+  if (!prm || prm->format != DMLC_AMD_LIBSVM) return 0;
+  const uint64_t b = dmlc_amd::exact_rec_bytes(ntiles, dmlc_amd::exact_rec_win(T, dmlc_amd::kWin), dmlc_amd::kThreads);
+  return dmlc_amd::exact_rec_on(nbytes, b) ? b : 0;
+}
+
 size_t dmlc_amd_workspace_bytes(uint64_t nbytes, int nchunks, const dmlc_amd_params *prm) {
   const uint64_t T = tile_of(prm);
   const uint64_t ntiles = (nbytes + T - 1) / T;
@@ -142,7 +151,7 @@ size_t dmlc_amd_workspace_bytes(uint64_t nbytes, int nchunks, const dmlc_amd_par
   const uint64_t nft = (nbytes + kFastTile - 1) / kFastTile;
   return (size_t)((2 * ntiles * kSlots + 2 * nc + nc * 8 + (nc + 1) + nft * 8 + dmlc_amd::kLabShards * 8) *
                       sizeof(uint64_t) +
-                  12 * 256);
+                  12 * 256 + rec_bytes_of(nbytes, T, ntiles, prm) + 2 * 256);
 }
 
 int dmlc_amd_parse(const void *d_text, uint64_t nbytes, const uint64_t *d_chunk_starts, int nchunks,
@@ -180,6 +189,11 @@ int dmlc_amd_parse(const void *d_text, uint64_t nbytes, const uint64_t *d_chunk_
   unsigned long long *ferr = cv.take<unsigned long long>(1);
   uint64_t *lb = cv.take<uint64_t>(nft * 8 + 1);
   uint64_t *labsum = cv.take<uint64_t>(dmlc_amd::kLabShards * 8);
+  const uint64_t recb = rec_bytes_of(nbytes, T, ntiles, prm);
+  const uint32_t rec_win = dmlc_amd::exact_rec_win(T, dmlc_amd::kWin);
+  uint64_t *rec_meta = recb ? cv.take<uint64_t>(ntiles * rec_win * 2) : nullptr;
+  uint32_t *rec = recb ? cv.take<uint32_t>(ntiles * rec_win * 4 * dmlc_amd::kThreads) : nullptr;
+  if (recb && (!rec || !rec_meta)) return DMLC_AMD_ERR_ARG;
   if (!tile_cnt || !tile_base || !chunk_min || !fast_min || !chunk_sink || !units || !ctl || !ferr || !lb || !labsum)
     return DMLC_AMD_ERR_ARG;
   // FillData's thread ranges become the units the kernels parse; the
@@ -227,6 +241,9 @@ int dmlc_amd_parse(const void *d_text, uint64_t nbytes, const uint64_t *d_chunk_
     a.chunk_min = chunk_min;
     a.err = reinterpret_cast<unsigned long long *>(res + 8);
     a.gate = ctl;
+    a.rec = rec;
+    a.rec_meta = rec_meta;
+    a.rec_win = rec ? rec_win : 0;
     dmlc_amd::FastSvmArgs f;
     std::memset(&f, 0, sizeof(f));
     f.text = a.text;
@@ -342,6 +359,9 @@ int dmlc_amd_parse(const void *d_text, uint64_t nbytes, const uint64_t *d_chunk_
     a.chunk_min = chunk_min;
     a.err = reinterpret_cast<unsigned long long *>(res + 8);
     a.gate = ctl;
+    a.rec = rec;
+    a.rec_meta = rec_meta;
+    a.rec_win = rec ? rec_win : 0;
     dmlc_amd::FastSvmArgs f;  // the single-pass kernel with the libfm roles (svm_fast.h)
     std::memset(&f, 0, sizeof(f));
     f.text = a.text;

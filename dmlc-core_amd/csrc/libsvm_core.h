@@ -212,27 +212,89 @@ DA_HDF void index_min(const LibsvmArgs &a, Src &src, const Seg &sg, uint32_t I, 
   }
 }
 
-// Write pass: emit the segment's rows and entries in text order at base +
-// the running local counts (I / V / Dg: the role masks of its start state).
+// Write pass: emit the segment's rows and entries at base + their rank in the
+// segment (I / V / Dg: the role masks of its start state).  One loop per
+// kind -- indices, values, rows -- so the lanes of a wave decode the same
+// kind together; a rank is a popcount of the mask below the position.
+DA_HD int chunk_at(const LibsvmArgs &a, int chunk, uint64_t x) {
+  while (x >= a.cs[chunk + 1]) ++chunk;
+  return chunk;
+}
 DA_HDF void emit(const LibsvmArgs &a, Src &src, const Seg &sg, uint32_t I, uint32_t V, uint32_t Dg,
                  const Base64 &base, const fast::DecTables *dt) {
-  Cnt cnt = cnt_zero();
-  uint32_t ev = sg.ls | I | V | Dg;
-  int chunk = sg.chunk;
-  uint64_t cfloor = a.cs[chunk], cend = a.cs[chunk + 1];
-  src.lim = a.lim(chunk);  // decoders read to the InputSplit chunk end
-  while (ev) {
-    const int i = ctz32(ev);
-    ev &= ev - 1;
-    const uint32_t bit = 1u << i;
-    const uint64_t x = sg.lo + i;
-    while (x >= cend) {  // entered the next chunk
-      ++chunk;
-      cfloor = a.cs[chunk];
-      cend = a.cs[chunk + 1];
-      src.lim = a.lim(chunk);
+  // ---- indices
+  {
+    int chunk = sg.chunk;
+    src.lim = a.lim(chunk);
+    uint64_t ir = base.c[C_INDEX];
+    for (uint32_t m = I; m; m &= m - 1, ++ir) {
+      const uint64_t x = sg.lo + ctz32(m);
+      if (x >= a.cs[chunk + 1]) {
+        chunk = chunk_at(a, chunk, x);
+        src.lim = a.lim(chunk);
+      }
+      uint64_t v;
+      if (!index_at(src, x, a.wide != 0, dt, &v)) {
+        raise_error(a.err, E_NEG_INDEX, x);
+        v = 0;
+      }
+      if (a.indexing_mode > 0 || (a.indexing_mode < 0 && a.chunk_min[chunk] > 0)) --v;
+      if (ir < a.cap[C_INDEX]) {
+        if (a.wide) reinterpret_cast<uint64_t *>(a.index)[ir] = v;
+        else reinterpret_cast<uint32_t *>(a.index)[ir] = (uint32_t)v;
+      } else {
+        raise_error(a.err, E_CAPACITY, x);
+      }
     }
-    if (sg.ls & bit) {
+  }
+  // ---- values (a run after "idx:", or ParsePair's value read at the line
+  // end after a dangling "idx:"; never both at one position)
+  {
+    int chunk = sg.chunk;
+    src.lim = a.lim(chunk);
+    uint64_t vr = base.c[C_VALUE];
+    for (uint32_t m = V | Dg; m; m &= m - 1, ++vr) {
+      const uint32_t i = (uint32_t)ctz32(m);
+      const uint64_t x = sg.lo + i;
+      if (x >= a.cs[chunk + 1]) {
+        chunk = chunk_at(a, chunk, x);
+        src.lim = a.lim(chunk);
+      }
+      bool nan_err = false;
+      float v;
+      if ((V >> i) & 1u) {
+#ifdef FSVM_ABL_EXNODEC  // timing ablation only (tools/build_variants.sh), never shipped
+        v = (float)(x & 7u);
+#else
+        v = value_at(src, x, dt, &nan_err);
+#endif
+      } else {
+        uint64_t e;
+        v = parse_float(src, x + 1, &e, &nan_err);
+      }
+      if (nan_err) raise_error(a.err, E_NAN_LITERAL, x);
+      if (vr < a.cap[C_VALUE]) a.value[vr] = v;
+      else raise_error(a.err, E_CAPACITY, x);
+    }
+  }
+  // ---- rows: label[:weight] [qid:n] heads, row offsets, unit table rows
+  if (sg.ls) {
+    Cnt cnt = cnt_zero();  // rows / labels / weights / qids so far in the segment
+    int chunk = sg.chunk;
+    uint64_t cfloor = a.cs[chunk], cend = a.cs[chunk + 1];
+    src.lim = a.lim(chunk);
+    for (uint32_t m = sg.ls; m; m &= m - 1) {
+      const uint32_t i = (uint32_t)ctz32(m);
+      const uint64_t x = sg.lo + i;
+      while (x >= cend) {
+        ++chunk;
+        cfloor = a.cs[chunk];
+        cend = a.cs[chunk + 1];
+        src.lim = a.lim(chunk);
+      }
+      const uint32_t below = (1u << i) - 1u;
+      cnt.c[C_INDEX] = (uint32_t)popc32(I & below);
+      cnt.c[C_VALUE] = (uint32_t)popc32((V | Dg) & below);
       const bool l0 = x == cfloor;
       if (l0) {
         uint64_t *row = a.chunk_tab + (uint64_t)chunk * 8;  // rows of 8 slots (dmlc_amd.h)
@@ -265,44 +327,6 @@ DA_HDF void emit(const LibsvmArgs &a, Src &src, const Seg &sg, uint32_t I, uint3
         cnt.c[C_WEIGHT] += h.w;
         cnt.c[C_QID] += h.q;
       }
-    }
-    if (I & bit) {
-      uint64_t v;
-      if (!index_at(src, x, a.wide != 0, dt, &v)) {
-        raise_error(a.err, E_NEG_INDEX, x);
-        v = 0;
-      }
-      if (a.indexing_mode > 0 || (a.indexing_mode < 0 && a.chunk_min[chunk] > 0)) --v;
-      const uint64_t ir = base.c[C_INDEX] + cnt.c[C_INDEX];
-      if (ir < a.cap[C_INDEX]) {
-        if (a.wide) reinterpret_cast<uint64_t *>(a.index)[ir] = v;
-        else reinterpret_cast<uint32_t *>(a.index)[ir] = (uint32_t)v;
-      } else {
-        raise_error(a.err, E_CAPACITY, x);
-      }
-      cnt.c[C_INDEX]++;
-    } else if (V & bit) {
-      const uint64_t vr = base.c[C_VALUE] + cnt.c[C_VALUE];
-      bool nan_err = false;
-#ifdef FSVM_ABL_EXNODEC  // timing ablation only (tools/build_variants.sh), never shipped
-      const float v = (float)(x & 7u);
-#else
-      const float v = value_at(src, x, dt, &nan_err);
-#endif
-      if (nan_err) raise_error(a.err, E_NAN_LITERAL, x);
-      if (vr < a.cap[C_VALUE]) a.value[vr] = v;
-      else raise_error(a.err, E_CAPACITY, x);
-      cnt.c[C_VALUE]++;
-    }
-    if (Dg & bit) {
-      const uint64_t vr = base.c[C_VALUE] + cnt.c[C_VALUE];
-      bool nan_err = false;
-      uint64_t e;
-      const float v = parse_float(src, x + 1, &e, &nan_err);
-      if (nan_err) raise_error(a.err, E_NAN_LITERAL, x);
-      if (vr < a.cap[C_VALUE]) a.value[vr] = v;
-      else raise_error(a.err, E_CAPACITY, x);
-      cnt.c[C_VALUE]++;
     }
   }
 }
@@ -366,7 +390,19 @@ DA_HDF void tile(const LibsvmArgs &a, Shared &sh, BK &bk, uint64_t k) {
   Src src;
   src.g = a.text;
   src.lds = sh.win;
+  // the count pass's records of this tile's windows (args.h LibsvmArgs.rec):
+  // the write pass takes the role masks and head counts from them instead of
+  // walking the window again
+  const bool recs = a.rec != nullptr;
+  uint32_t *rec_t = recs ? a.rec + (uint64_t)k * a.rec_win * 4 * kThreads : nullptr;
+  uint64_t *meta_t = recs ? a.rec_meta + (uint64_t)k * a.rec_win * 2 : nullptr;
   while (!done) {
+    const bool from_rec = MODE == 2 && recs && (uint32_t)j < a.rec_win;
+    if (MODE == 2 && recs && (uint32_t)j == a.rec_win) {  // the first window past the records
+      st0 = (uint32_t)meta_t[(j - 1) * 2 + 1];
+      if (tid == 0) sh.pending[(j + 1) & 1] = meta_t[(j - 1) * 2];
+      bk.sync();
+    }
     const uint64_t pend = sh.pending[(j + 1) & 1];  // written during window j-1
     uint64_t wend = mn(w0 + (uint64_t)kWin, a.n);
     if (wend == a.n) done = true;
@@ -432,7 +468,7 @@ DA_HDF void tile(const LibsvmArgs &a, Shared &sh, BK &bk, uint64_t k) {
     // ---- head sections -> R1 marks, and the segment's row / weight / qid
     // counts (libsvm_parser.h:99-132)
     uint32_t hrow = 0, hw = 0, hq = 0;
-    if (sg.ls) {
+    if (sg.ls && !from_rec) {
       uint32_t m = sg.ls;
       int chunk = sg.chunk;
       while (m) {
@@ -456,16 +492,41 @@ DA_HDF void tile(const LibsvmArgs &a, Shared &sh, BK &bk, uint64_t k) {
     bk.sync();
 
     // ---- role masks and transition function of my segment, then block scan
-    uint32_t fn = kIdentityFn;
-    Roles R;
-    if (sg.lo < sg.hi) walk_roles(a, src, sh.r1bits, w0, sg, fn, R);
-    else
-      for (int s2 = 0; s2 < 4; ++s2) R.idx[s2] = R.val[s2] = R.dng[s2] = 0;
-    uint32_t fn_total;
-    const uint32_t fn_ex = bk.exclusive(fn, kIdentityFn, FnCompose(), &fn_total);
-    const uint32_t st = (fn_ex >> (2 * st0)) & 3u;
-    const uint32_t st_next = (fn_total >> (2 * st0)) & 3u;
-    const uint32_t I = pick(R.idx, st), V = pick(R.val, st), Dg = pick(R.dng, st);
+    // (or the count pass's record of them)
+    uint32_t I, V, Dg, st_next = S_PRE;
+    uint32_t *rw = recs && (uint32_t)j < a.rec_win ? rec_t + (uint64_t)j * 4 * kThreads : nullptr;
+    if (from_rec) {
+      I = rw[tid];
+      V = rw[kThreads + tid];
+      Dg = rw[2 * kThreads + tid];
+      const uint32_t hc = rw[3 * kThreads + tid];
+      hrow = hc & 0xFFu;
+      hw = (hc >> 8) & 0xFFu;
+      hq = hc >> 16;
+    } else {
+      uint32_t fn = kIdentityFn;
+      Roles R;
+      if (sg.lo < sg.hi) walk_roles(a, src, sh.r1bits, w0, sg, fn, R);
+      else
+        for (int s2 = 0; s2 < 4; ++s2) R.idx[s2] = R.val[s2] = R.dng[s2] = 0;
+      uint32_t fn_total;
+      const uint32_t fn_ex = bk.exclusive(fn, kIdentityFn, FnCompose(), &fn_total);
+      const uint32_t st = (fn_ex >> (2 * st0)) & 3u;
+      st_next = (fn_total >> (2 * st0)) & 3u;
+      I = pick(R.idx, st);
+      V = pick(R.val, st);
+      Dg = pick(R.dng, st);
+      if (MODE == 1 && rw) {  // the record for the write pass
+        rw[tid] = I;
+        rw[kThreads + tid] = V;
+        rw[2 * kThreads + tid] = Dg;
+        rw[3 * kThreads + tid] = hrow | (hw << 8) | (hq << 16);
+        if (tid == 0) {
+          meta_t[j * 2] = sh.pending[j & 1];  // (set by the heads, before the scan's barriers)
+          meta_t[j * 2 + 1] = st_next;
+        }
+      }
+    }
 
     // ---- counts by popcount, then (write pass) scan + emit
     Cnt c = zero;

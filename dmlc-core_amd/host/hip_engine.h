@@ -353,6 +353,10 @@ struct EngineConfig {
   // "h2d_kernel" / "d2h_kernel": one direction by kernel, the other by DMA
   // (the SDMA engines and the copy kernels then carry different directions).
   enum CopyMode { kKernel, kDma, kH2DKernel, kD2HKernel } copy_mode = kKernel;
+  // DMLC_AMD_PRECOPY=0: the CSR copy-out waits for the parse's result on the
+  // host (sizes exact) instead of being queued behind the parse with sizes
+  // read on the device (dmlc_amd_copy_n_dev) -- for A/B timing
+  bool precopy = true;
   bool h2d_kernel() const { return copy_mode == kKernel || copy_mode == kH2DKernel; }
   bool d2h_kernel() const { return copy_mode == kKernel || copy_mode == kD2HKernel; }
 
@@ -362,6 +366,7 @@ struct EngineConfig {
     batch_bytes = env_bytes("DMLC_AMD_BATCH_BYTES", batch_bytes, 1u << 20);
     if (const char *w = std::getenv("DMLC_AMD_WORKERS")) per_device = std::max(1, std::atoi(w));
     if (const char *st = std::getenv("DMLC_AMD_STATS")) stats = std::atoi(st) != 0;
+    if (const char *pc = std::getenv("DMLC_AMD_PRECOPY")) precopy = std::atoi(pc) != 0;
     if (const char *c = std::getenv("DMLC_AMD_COPY")) {
       const std::string v(c);
       if (v == "kernel") copy_mode = kKernel;
@@ -680,7 +685,7 @@ class HipTextParser : public dmlc::Parser<IndexType, DType> {
       Outputs(w, want, &out);
       CheckRc(dmlc_amd_parse(d_text, b->bytes, d_cs, nch, &p, &out, d_tab, d_ws, ws,
                              reinterpret_cast<dmlc_amd_result *>(d_res), s));
-      pre = attempt == 0 && cfg_.d2h_kernel() && w->est[0] > 0;
+      pre = attempt == 0 && cfg_.precopy && cfg_.d2h_kernel() && w->est[0] > 0;
       if (pre) {
         const void *src[8] = {out.offset, out.label, out.weight, out.qid, out.index, out.field, out.value, d_tab};
         pre_dst[0] = b->off.reserve(w->est[0] / 8 + 1);

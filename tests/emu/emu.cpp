@@ -246,6 +246,18 @@ extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *c
     a.chunk_min = chunk_min.data();
     a.err = err;
     a.gate = &gate;
+    std::vector<uint32_t> rec;  // the exact libsvm kernels' count-pass records (capi.cpp)
+    std::vector<uint64_t> rec_meta;
+    if (!fm) {
+      const uint32_t rw = exact_rec_win(T, kWin);
+      if (exact_rec_on(nbytes, exact_rec_bytes(ntiles, rw, kThreads))) {
+        rec.assign(ntiles * rw * 4 * kThreads, 0xCDCDCDCDu);  // device memory is not zeroed either
+        rec_meta.assign(ntiles * rw * 2, 0xCDCDCDCDCDCDCDCDull);
+        a.rec = rec.data();
+        a.rec_meta = rec_meta.data();
+        a.rec_win = rw;
+      }
+    }
     if (use_fast) {
       FastSvmArgs f;
       std::memset(&f, 0, sizeof(f));

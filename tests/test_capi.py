@@ -52,8 +52,15 @@ def test_workspace_and_argument_validation(lib):
     p = dmlc_amd.make_params("libsvm")
     ws = dmlc_amd.lib().dmlc_amd_workspace_bytes(1 << 30, 128, ctypes.byref(p))
     tile, _ = dmlc_amd.fast_geometry()
-    # per single-pass tile a look-back record (8 words), plus per-chunk and per-exact-tile tables
-    assert 0 < ws < (1 << 30) // tile * 64 + (1 << 20)
+    # per single-pass tile a look-back record (8 words), plus per-chunk and per-exact-tile tables,
+    # plus the exact libsvm count pass's window records (args.h exact_rec_bytes: at most the
+    # text's size + 64 MiB, about half of it at the default 256 KiB exact tiles)
+    assert 0 < ws < (1 << 30) // tile * 64 + (1 << 20) + (1 << 30) * 6 // 10
+    c = dmlc_amd.make_params("csv")
+    wc = dmlc_amd.lib().dmlc_amd_workspace_bytes(1 << 30, 128, ctypes.byref(c))
+    assert 0 < wc < (1 << 30) // tile * 64 + (1 << 20)  # (no records for CSV)
+    small = dmlc_amd.make_params("libsvm", tile_bytes=64)  # tiny exact tiles: records off
+    assert dmlc_amd.lib().dmlc_amd_workspace_bytes(1 << 30, 128, ctypes.byref(small)) < (1 << 30) * 2
     # bad index_bits is rejected before any device work
     bad = dmlc_amd.make_params("libsvm", index_bits=16)
     csr = dmlc_amd.Csr()

@@ -10,12 +10,12 @@ export TMPDIR=${TMPDIR:-/tmp}
 for m in ${MODES:-kernel}; do
 for w in ${WORKERS:-2 3 4}; do
   for b in ${BATCHES:-33554432 67108864}; do
-    t=${m}_w${w}_b${b}
-    DMLC_AMD_COPY=$m DMLC_AMD_WORKERS=$w DMLC_AMD_BATCH_BYTES=$b timeout -k 10 300 python tools/e2e/run_e2e.py ${CONFIGS:-libsvm_1m_x128} > $O/e2e_$t.jsonl 2> $O/e2e_$t.err || { tail -3 $O/e2e_$t.err; exit 1; }
+    t=${m}_w${w}_b${b}_p${PRECOPY:-1}
+    DMLC_AMD_PRECOPY=${PRECOPY:-1} DMLC_AMD_COPY=$m DMLC_AMD_WORKERS=$w DMLC_AMD_BATCH_BYTES=$b timeout -k 10 300 python tools/e2e/run_e2e.py ${CONFIGS:-libsvm_1m_x128} > $O/e2e_$t.jsonl 2> $O/e2e_$t.err || { tail -3 $O/e2e_$t.err; exit 1; }
     python3 -c "
 import json
 for l in open('$O/e2e_$t.jsonl'):
-    d=json.loads(l); print('copy $m workers $w batch $b', d['config'], d.get('GBps'), d.get('stages'))"
+    d=json.loads(l); print('copy $m workers $w batch $b precopy ${PRECOPY:-1}', d['config'], d.get('GBps'), d.get('stages'))"
   done
 done
 done
