@@ -78,6 +78,31 @@ DA_HD Field decode_field(const Src &at, int vtype, uint64_t p, const fast::DecTa
   return r;
 }
 
+// Whether decode_field at p consumes a byte (endptr != p: the field holds a
+// value, csv_parser.h:115-118) without decoding it -- the count pass needs
+// no more for a value column.  ParseFloat (strtonum.h:95-264) consumes
+// leading isspace bytes, a sign, "inf" / "infinity" / "nan" (any case; 3 or 8
+// letters of infinity), digits, '.', an exponent 'e' / 'E' or the 'f' suffix;
+// strtoll (base 0) consumes only when a decimal digit follows the optional
+// blanks and sign (a "0x" prefix starts with one).
+DA_HD bool field_consumed(const Src &at, int vtype, uint64_t p) {
+  uint32_t c = at(p);
+  if (vtype != 0) {
+    while (is_cspace(c)) c = at(++p);
+    if (c == '-' || c == '+') c = at(++p);
+    return is_digit(c);
+  }
+  if (is_space(c) || c == '-' || c == '+' || is_digit(c) || c == '.' || (c | 32u) == 'e' || (c | 32u) == 'f')
+    return true;
+  if ((c | 32u) == 'n')
+    return ((at(p + 1) | 32u) & 0xFFu) == 'a' && ((at(p + 2) | 32u) & 0xFFu) == 'n';
+  if ((c | 32u) != 'i') return false;
+  const char kInf[8] = {'i', 'n', 'f', 'i', 'n', 'i', 't', 'y'};
+  int i = 1;
+  while (i < 8 && ((at(p + i) | 32u) & 0xFFu) == (uint32_t)kInf[i]) ++i;
+  return i == 3 || i == 8;
+}
+
 // csv_parser.h:81-145 for ONE line starting at `lbegin` (a CSV line start).
 template <int MODE>
 DA_HDF void csv_line_seq(const Src &at, const CsvArgs &a, uint64_t lbegin, uint64_t end, Cnt &cnt,
@@ -220,9 +245,17 @@ DA_HDF void walk(const CsvArgs &a, Src &src, const Seg &sg, uint32_t state, Cnt 
     }
     if (!in_line || slow) continue;
     if ((sg.fs >> i) & 1u) {
-      Field f = decode_field(src, a.vtype, x, dt);
-      if (MODE == 2 && f.nan_err) raise_error(a.err, E_NAN_LITERAL, x);
       const bool vc = is_value_col(a, col);
+      Field f;
+      if (MODE == 2 || (!vc && (int64_t)col != a.label_column)) {  // (the count pass decodes weights only)
+        f = decode_field(src, a.vtype, x, dt);
+      } else {
+        f.f = 0.f;
+        f.i = 0;
+        f.nan_err = false;
+        f.end = vc && field_consumed(src, a.vtype, x) ? x + 1 : x;
+      }
+      if (MODE == 2 && f.nan_err) raise_error(a.err, E_NAN_LITERAL, x);
       if ((int64_t)col == a.label_column) {
         if (MODE == 2) {
           const uint64_t r = base.c[C_LABEL] + cnt.c[C_LABEL];

@@ -8,6 +8,7 @@
 #include <string>
 
 #include "fast_common.h"
+#include "csv_core.h"
 #include "libsvm_core.h"
 
 using namespace dmlc_amd;
@@ -90,7 +91,7 @@ int main(int argc, char **argv) {
   long ex_f = 0, ex_c = 0;
   for (long it = 0; it < n; ++it) {
     std::string s;
-    const char *head = (it & 1) ? "0123456789+-.eE" : "0123456789+-.eE a,\n\tiInN";
+    const char *head = (it & 1) ? "0123456789+-.eE" : "0123456789+-.eE a,\n\tiInNfF\v\f\rx";
     s += head[rnd() % strlen(head)];
     const char *al = "0123456789012345678901234567890123456789..eE+-infaINFANx :#\t";
     const int m = (int)(rnd() % 24);
@@ -129,6 +130,12 @@ int main(int argc, char **argv) {
           if (bad++ < 10) printf("csv mismatch '%.24s' win=%.9g end %llu byte=%.9g end %llu\n", s.c_str(), cv,
                                  (unsigned long long)ce, r, (unsigned long long)e);
         }
+      }
+    }
+    for (int vt = 0; vt < 3; ++vt) {  // CSV count pass: field_consumed == (decode_field's end != p)
+      const csv::Field f = csv::decode_field(src, vt, 0);
+      if (csv::field_consumed(src, vt, 0) != (f.end != 0)) {
+        if (bad++ < 10) printf("consumed mismatch vt %d '%.24s'\n", vt, s.c_str());
       }
     }
     for (int wide = 0; wide < 2; ++wide) {
