@@ -183,6 +183,11 @@ struct CsvArgs {
   const uint32_t *gate;  // when set, the tile kernels run only if *gate != 0
   UnitLim ul;            // decoder limit per unit
   DA_HD uint64_t lim(int unit) const { return ul.lim(unit); }
+  // the count pass's per-thread window counts for the write pass (NULL: it
+  // counts again): [ntiles][rec_win][4][kThreads] words -- rows, values
+  // (= indices), labels, weights
+  uint32_t *rec;
+  uint32_t rec_win;
 };
 
 }  // namespace dmlc_amd

@@ -136,10 +136,10 @@ const char *dmlc_amd_error_string(int code) {
 int units_per_chunk(const dmlc_amd_params *p) { return p && p->nthread > 1 ? p->nthread : 1; }
 constexpr int kMaxNthread = 1 << 12;
 
-// the exact libsvm kernels' count-pass records (args.h exact_rec_*): bytes,
-// 0 when the format has none or they would outgrow the text
+// the exact libsvm / CSV kernels' count-pass records (args.h exact_rec_*):
+// bytes, 0 when the format has none or they would outgrow the text
 uint64_t rec_bytes_of(uint64_t nbytes, uint64_t T, uint64_t ntiles, const dmlc_amd_params *prm) {
-  if (!prm || prm->format != DMLC_AMD_LIBSVM) return 0;
+  if (!prm || prm->format == DMLC_AMD_LIBFM) return 0;
   const uint64_t b = dmlc_amd::exact_rec_bytes(ntiles, dmlc_amd::exact_rec_win(T, dmlc_amd::kWin), dmlc_amd::kThreads);
   return dmlc_amd::exact_rec_on(nbytes, b) ? b : 0;
 }
@@ -300,6 +300,8 @@ int dmlc_amd_parse(const void *d_text, uint64_t nbytes, const uint64_t *d_chunk_
     a.chunk_tab = d_chunk_table ? d_chunk_table : chunk_sink;
     a.err = reinterpret_cast<unsigned long long *>(res + 8);
     a.gate = ctl;
+    a.rec = rec;
+    a.rec_win = rec ? rec_win : 0;
     dmlc_amd::FastCsvArgs f;
     std::memset(&f, 0, sizeof(f));
     f.text = a.text;

@@ -350,6 +350,7 @@ DA_HDF void tile(const CsvArgs &a, Shared &sh, BK &bk, uint64_t k) {
     return;
   }
   uint32_t col0 = 0;  // column state at the window start (window 0 starts at a line start)
+  uint32_t j = 0;     // window counter
   bool done = false;
   Src src;
   src.g = a.text;
@@ -445,7 +446,23 @@ DA_HDF void tile(const CsvArgs &a, Shared &sh, BK &bk, uint64_t k) {
     Base64 nob;
     for (int i = 0; i < C_N; ++i) nob.c[i] = 0;
     Cnt cc = zero;
-    if (sg.lo < sg.hi) walk<1>(a, src, sg, in_state, cc, nob, dtp);
+    // the count pass records each thread's window counts; the write pass
+    // takes them instead of counting again (args.h CsvArgs.rec)
+    uint32_t *rw = a.rec && j < a.rec_win ? a.rec + ((uint64_t)k * a.rec_win + j) * 4 * kThreads : nullptr;
+    if (MODE == 2 && rw) {
+      cc.c[C_ROWS] = rw[tid];
+      cc.c[C_INDEX] = cc.c[C_VALUE] = rw[kThreads + tid];
+      cc.c[C_LABEL] = rw[2 * kThreads + tid];
+      cc.c[C_WEIGHT] = rw[3 * kThreads + tid];
+    } else {
+      if (sg.lo < sg.hi) walk<1>(a, src, sg, in_state, cc, nob, dtp);
+      if (MODE == 1 && rw) {
+        rw[tid] = cc.c[C_ROWS];
+        rw[kThreads + tid] = cc.c[C_VALUE];
+        rw[2 * kThreads + tid] = cc.c[C_LABEL];
+        rw[3 * kThreads + tid] = cc.c[C_WEIGHT];
+      }
+    }
     if (MODE == 1) {
       mine = CntAdd()(mine, cc);
     } else {
@@ -461,6 +478,7 @@ DA_HDF void tile(const CsvArgs &a, Shared &sh, BK &bk, uint64_t k) {
     }
     col0 = next0 & 0x7FFFFFFFu;
     w0 = wend;
+    ++j;
     bk.sync();
   }
   if (MODE == 1) {

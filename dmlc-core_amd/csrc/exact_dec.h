@@ -102,4 +102,25 @@ DA_HD bool csv_value_at(const Src &src, uint64_t x, const fast::DecTables *dt, f
   return true;
 }
 
+// Digitchar (strtonum.h:70-72) and newline masks of the len <= 32 staged
+// bytes at win + off: nine aligned LDS words funnel-shifted to the segment,
+// classified four bytes at a time by the nibble tables (fast_common.h
+// classify_dword; bytes >= 0x80 are neither) -- instead of 32 byte reads.
+// The window buffer must hold 36 bytes past off.
+DA_HD void seg_masks(const uint8_t *win, uint32_t off, int len, uint32_t *dm, uint32_t *nl) {
+  const uint32_t *q = reinterpret_cast<const uint32_t *>(win + (off & ~3u));
+  const uint32_t sh = 8u * (off & 3u);
+  uint32_t v[9];
+  for (int i = 0; i < 9; ++i) v[i] = q[i];
+  uint32_t d = 0, n = 0;
+  for (int i = 0; i < 8; ++i) {
+    const fast::Nib b = fast::classify_dword(fast::funnel(v[i + 1], v[i], sh));
+    d |= (b.d & ~b.hi) << (4 * i);
+    n |= (b.n & ~b.hi) << (4 * i);
+  }
+  const uint32_t m = len >= 32 ? ~0u : ((1u << len) - 1u);
+  *dm = d & m;
+  *nl = n & m;
+}
+
 }  // namespace dmlc_amd

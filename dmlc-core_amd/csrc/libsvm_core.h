@@ -445,13 +445,9 @@ DA_HDF void tile(const LibsvmArgs &a, Shared &sh, BK &bk, uint64_t k) {
     if (sg.lo < sg.hi) {
       sg.chunk = chunk_of(a.cs, a.nchunk, sg.lo);
       src.lim = a.lim(sg.chunk);
-      uint32_t dm = 0, nl = 0, csm = 0;
+      uint32_t dm, nl, csm = 0;
       const int len = (int)(sg.hi - sg.lo);
-      for (int i = 0; i < len; ++i) {
-        const uint32_t c = sh.win[sg.lo + i - abase];
-        dm |= (uint32_t)is_digitchar(c) << i;
-        nl |= (uint32_t)is_nl(c) << i;
-      }
+      seg_masks(sh.win, (uint32_t)(sg.lo - abase), len, &dm, &nl);
       for (int c = sg.chunk; c < a.nchunk && a.cs[c] < sg.hi; ++c)
         if (a.cs[c] >= sg.lo) csm |= 1u << (a.cs[c] - sg.lo);
       const uint32_t prev = (sg.lo > 0 && !(csm & 1u) && is_digitchar(src(sg.lo - 1))) ? 1u : 0u;

@@ -53,6 +53,23 @@ int main(int argc, char **argv) {
     init_dec_tables(tb, b);
   }
   long fast_f = 0, fast_i = 0, bad = 0;
+  {  // exact kernels' segment masks (exact_dec.h seg_masks) against the byte classes
+    uint8_t win[64 + 40];
+    for (int it = 0; it < 20000; ++it) {
+      for (auto &c : win) c = (uint8_t)(rnd() % 4 ? "0123456789+-.eE \n\r:#xq"[rnd() % 22] : rnd() % 256);
+      const uint32_t off = (uint32_t)(rnd() % 40);
+      const int len = 1 + (int)(rnd() % 32);
+      uint32_t dm, nl, rd = 0, rn = 0;
+      seg_masks(win, off, len, &dm, &nl);
+      for (int i = 0; i < len; ++i) {
+        rd |= (uint32_t)is_digitchar(win[off + i]) << i;
+        rn |= (uint32_t)is_nl(win[off + i]) << i;
+      }
+      if (dm != rd || nl != rn) {
+        if (bad++ < 10) printf("seg_masks mismatch off %u len %d\n", off, len);
+      }
+    }
+  }
   for (long it = 0; it < n; ++it) {
     std::string s = gen();
     s += " :\n"[rnd() % 3];

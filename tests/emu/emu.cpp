@@ -369,6 +369,15 @@ extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *c
     for (int i = 0; i < 8; ++i) a.cap[i] = out->cap[i];
     a.chunk_tab = chunk_table ? chunk_table : sink.data();
     a.err = err;
+    std::vector<uint32_t> rec;  // the exact CSV kernels' count-pass records (capi.cpp)
+    {
+      const uint32_t rw = exact_rec_win(T, kWin);
+      if (exact_rec_on(nbytes, exact_rec_bytes(ntiles, rw, kThreads))) {
+        rec.assign(ntiles * rw * 4 * kThreads, 0xCDCDCDCDu);
+        a.rec = rec.data();
+        a.rec_win = rw;
+      }
+    }
     // mirrors launch_csv (csv.hip): uniform-grammar kernel first, exact tile
     // kernels when it sets the gate (or the parameters are outside its form)
     const bool cols_ok = prm->value_type == DMLC_AMD_F32 ? csv_fast_columns_ok(prm->label_column, prm->weight_column)

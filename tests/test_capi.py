@@ -56,9 +56,12 @@ def test_workspace_and_argument_validation(lib):
     # plus the exact libsvm count pass's window records (args.h exact_rec_bytes: at most the
     # text's size + 64 MiB, about half of it at the default 256 KiB exact tiles)
     assert 0 < ws < (1 << 30) // tile * 64 + (1 << 20) + (1 << 30) * 6 // 10
-    c = dmlc_amd.make_params("csv")
+    c = dmlc_amd.make_params("csv")  # (CSV keeps window count records too)
     wc = dmlc_amd.lib().dmlc_amd_workspace_bytes(1 << 30, 128, ctypes.byref(c))
-    assert 0 < wc < (1 << 30) // tile * 64 + (1 << 20)  # (no records for CSV)
+    assert 0 < wc < (1 << 30) // tile * 64 + (1 << 20) + (1 << 30) * 6 // 10
+    fm = dmlc_amd.make_params("libfm")
+    wf = dmlc_amd.lib().dmlc_amd_workspace_bytes(1 << 30, 128, ctypes.byref(fm))
+    assert 0 < wf < (1 << 30) // tile * 64 + (1 << 20)  # (no records for libfm)
     small = dmlc_amd.make_params("libsvm", tile_bytes=64)  # tiny exact tiles: records off
     assert dmlc_amd.lib().dmlc_amd_workspace_bytes(1 << 30, 128, ctypes.byref(small)) < (1 << 30) * 2
     # bad index_bits is rejected before any device work
