@@ -343,7 +343,7 @@ struct EngineConfig {
   int depth = 0;             // parsed batches ahead of the consumer (0: 2 per worker)
   bool max_index = false;    // reduce index/field maxima on the device (RowBlockIter::NumCol)
   bool stats = false;        // DMLC_AMD_STATS=1: per-stage times on stderr when the parser ends
-  // H2D / D2H (DMLC_AMD_COPY): "kernel" (default): the text by dmlc_amd_copy,
+  // H2D / D2H (DMLC_AMD_COPY): "kernel": the text by dmlc_amd_copy,
   // the batch's CSR arrays by one dmlc_amd_copy_n launch; "dma": one
   // hipMemcpyAsync per array.  (Measured on the MI355X box, DESIGN.md 5.2:
   // kernel copies 27 GB/s end to end, DMA 17 GB/s, and DMA with the CSR
@@ -352,7 +352,9 @@ struct EngineConfig {
   // tools/e2e/link_probe.py)
   // "h2d_kernel" / "d2h_kernel": one direction by kernel, the other by DMA
   // (the SDMA engines and the copy kernels then carry different directions).
-  enum CopyMode { kKernel, kDma, kH2DKernel, kD2HKernel } copy_mode = kKernel;
+  // Default "d2h_kernel" (round 4: 28.8-30.3 GB/s against 25.7-28.4 for
+  // "kernel" over two sweeps on config 2, gpurun_out/e2e_sweep_r4*.txt).
+  enum CopyMode { kKernel, kDma, kH2DKernel, kD2HKernel } copy_mode = kD2HKernel;
   // DMLC_AMD_PRECOPY=0: the CSR copy-out waits for the parse's result on the
   // host (sizes exact) instead of being queued behind the parse with sizes
   // read on the device (dmlc_amd_copy_n_dev) -- for A/B timing
