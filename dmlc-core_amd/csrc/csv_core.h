@@ -200,11 +200,14 @@ DA_HD bool is_value_col(const CsvArgs &a, uint64_t c) {
 template <int MODE>  // 1 count, 2 emit
 DA_HDF void walk(const CsvArgs &a, Src &src, const Seg &sg, uint32_t state, Cnt &cnt,
                      const Base64 &base, const fast::DecTables *dt) {
-  uint32_t ev = sg.ls | sg.dl | sg.fs;
+  // events: line and field starts; a field's column is the delimiters since
+  // its line start, a popcount (col0 at bit `from`)
+  uint32_t ev = sg.ls | sg.fs;
   int chunk = sg.chunk;
   uint64_t cend = a.cs[chunk + 1];
   src.lim = a.lim(chunk);  // decoders read to the InputSplit chunk end
-  uint64_t col = state & 0x3FFFFFFFu;
+  uint64_t col0 = state & 0x3FFFFFFFu;
+  uint32_t from_mask = 0;  // bits below the current line's start
   bool slow = (state >> 30) & 1u;
   bool in_line = (state >> 31) & 1u;  // a line start has been seen (always true inside an extent)
   while (ev) {
@@ -218,7 +221,8 @@ DA_HDF void walk(const CsvArgs &a, Src &src, const Seg &sg, uint32_t state, Cnt 
     }
     if ((sg.ls >> i) & 1u) {
       in_line = true;
-      col = 0;
+      col0 = 0;
+      from_mask = (1u << i) - 1u;
       slow = (sg.slow >> i) & 1u;
       // the chunk's first line: only newlines lie between its start and x
       // (a chunk row is the exclusive count at the chunk start, dmlc_amd.h)
@@ -245,6 +249,7 @@ DA_HDF void walk(const CsvArgs &a, Src &src, const Seg &sg, uint32_t state, Cnt 
     }
     if (!in_line || slow) continue;
     if ((sg.fs >> i) & 1u) {
+      const uint64_t col = col0 + (uint32_t)popc32(sg.dl & ((1u << i) - 1u) & ~from_mask);
       const bool vc = is_value_col(a, col);
       Field f;
       if (MODE == 2 || (!vc && (int64_t)col != a.label_column)) {  // (the count pass decodes weights only)
@@ -295,7 +300,6 @@ DA_HDF void walk(const CsvArgs &a, Src &src, const Seg &sg, uint32_t state, Cnt 
         if (p >= cend || is_nl(src(p))) raise_error(a.err, E_CSV_DELIM, p);
       }
     }
-    if ((sg.dl >> i) & 1u) ++col;
   }
 }
 
@@ -398,12 +402,8 @@ DA_HDF void tile(const CsvArgs &a, Shared &sh, BK &bk, uint64_t k) {
       int c = sg.chunk;
       src.lim = a.lim(c);
       const int len = (int)(sg.hi - sg.lo);
-      uint32_t nl = 0, dl = 0, ls = 0;
-      for (int i = 0; i < len; ++i) {
-        const uint32_t ch = sh.win[sg.lo + i - abase];
-        nl |= (uint32_t)is_nl(ch) << i;
-        dl |= (uint32_t)(ch == a.delim) << i;
-      }
+      uint32_t nl, dl, ls = 0;
+      seg_masks_csv(sh.win, (uint32_t)(sg.lo - abase), len, a.delim, &nl, &dl);
       // line starts: non-nl byte after an nl byte (or a chunk start), minus absorbed
       const uint32_t prev_nl = (sg.lo == 0 || is_nl(src(sg.lo - 1))) ? 1u : 0u;
       uint32_t cand = ~nl & ((nl << 1) | prev_nl);

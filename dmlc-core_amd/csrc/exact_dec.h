@@ -123,4 +123,29 @@ DA_HD void seg_masks(const uint8_t *win, uint32_t off, int len, uint32_t *dm, ui
   *nl = n & m;
 }
 
+// Newline and delimiter masks of the len <= 32 staged bytes at win + off (the
+// CSV exact kernels): byte-equality by the carry-free zero-byte test on nine
+// aligned LDS words, four bytes at a time.
+DA_HD uint32_t eq_nib(uint32_t x, uint32_t rep) {  // 4 bits: byte i of x == the byte repeated in rep
+  const uint32_t t = x ^ rep;
+  const uint32_t nz = (((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u;  // bit 7: byte nonzero
+  return ((((~nz >> 7) & 0x01010101u) * 0x01020408u) >> 24) & 0xFu;
+}
+DA_HD void seg_masks_csv(const uint8_t *win, uint32_t off, int len, uint32_t delim, uint32_t *nl, uint32_t *dl) {
+  const uint32_t *q = reinterpret_cast<const uint32_t *>(win + (off & ~3u));
+  const uint32_t sh = 8u * (off & 3u);
+  const uint32_t rd = (delim & 0xFFu) * 0x01010101u;
+  uint32_t v[9];
+  for (int i = 0; i < 9; ++i) v[i] = q[i];
+  uint32_t n = 0, d = 0;
+  for (int i = 0; i < 8; ++i) {
+    const uint32_t x = fast::funnel(v[i + 1], v[i], sh);
+    n |= (eq_nib(x, 0x0A0A0A0Au) | eq_nib(x, 0x0D0D0D0Du)) << (4 * i);
+    d |= eq_nib(x, rd) << (4 * i);
+  }
+  const uint32_t m = len >= 32 ? ~0u : ((1u << len) - 1u);
+  *nl = n & m;
+  *dl = d & m;
+}
+
 }  // namespace dmlc_amd

@@ -270,57 +270,6 @@ struct Tile {
   }
 };
 
-// qid_ok from the classification planes, for the qid run starting at bit qb
-// of segment tid (planes D, N, C, QM of it in registers, the segment before
-// it from LDS): 1 ok, 0 not, 2 undecided here (the run or the line head
-// reaches past these 128 bytes, a chunk start lies before the run in the
-// segment, or the head is label:weight, whose tab rule needs the bytes) --
-// the byte walk (Tile::qid_ok) decides then.  Blanks are the bytes of no
-// plane (qid_clean turned the token letters into blanks).
-DA_HD int hi_below(uint64_t lo, uint64_t hi, int e) {  // highest set position < e of the 128 bits, or -1
-  if (e > 64) {
-    const uint64_t h = hi & (e >= 128 ? ~0ull : ((1ull << (e - 64)) - 1));
-    if (h) return 127 - clz64(h);
-    e = 64;
-  }
-  const uint64_t l = lo & (e >= 64 ? ~0ull : ((1ull << e) - 1));
-  return l ? 63 - clz64(l) : -1;
-}
-DA_HD int qid_head_planes(const Tile &t, int tid, uint64_t P, uint32_t qb, uint64_t D, uint64_t N, uint64_t C,
-                          uint64_t QM, uint64_t S, uint64_t F) {
-  const uint32_t r = (uint32_t)ctz64(~(D >> qb));  // the digitchar run at qb
-  if (qb + r >= 64) return 2;
-  const uint64_t G = (uint64_t)t.sh->gw[2 * tid] | ((uint64_t)t.sh->gw[2 * tid + 1] << 32);
-  if (r > 18 || ((~G >> qb) & ((1ull << r) - 1))) return 0;  // 1-18 plain digits (atoll)
-  if (S & ((2ull << qb) - 1)) return 2;
-  const uint64_t pd = t.sh->u.m.d[tid], pn = t.sh->u.m.n[tid], pc = t.sh->u.m.c[tid];
-  const uint64_t Blo = ~(pd | pn | pc), Bhi = ~(D | N | C | QM);
-  const uint64_t Nlo = pn & ~pc, Clo = pc;  // (':' or a qid marker: both undecided)
-  const int64_t base = (int64_t)P - 64;
-  const int64_t lo_st = t.tlo >= (uint64_t)kPre ? (int64_t)(t.tlo - kPre) : 0;
-  const int64_t lim = (int64_t)F > lo_st ? (int64_t)F : lo_st;
-  const int limp = lim >= base ? (int)(lim - base) : -1, w = limp >= 0 ? limp : 0;
-  const int Fp = (int64_t)F >= base ? (int)((int64_t)F - base) : -1;
-  auto bit = [](uint64_t lo, uint64_t hi, int p) { return ((p >= 64 ? hi >> (p - 64) : lo >> p) & 1u) != 0; };
-  auto skip = [&](uint64_t Mlo, uint64_t Mhi, int e) {  // the run of M bytes ending at e, down to the wall
-    const int q = hi_below(~Mlo, ~Mhi, e) + 1;
-    return q > w ? q : w;
-  };
-  int e = skip(Blo, Bhi, 64 + (int)qb - 4);  // blanks before the token
-  if (e == 0 && limp < 0) return 2;
-  if (e == limp || !bit(pd, D, e - 1)) return 0;  // no run before the token
-  e = skip(pd, D, e);
-  if (e == 0 && limp < 0) return 2;
-  if (e == Fp) return 1;  // the line's label
-  e = skip(Blo, Bhi, e);
-  if (e == Fp) return 1;
-  if (e == 0 && limp < 0) return 2;
-  if (e == limp) return 0;
-  if (bit(Nlo, N, e - 1)) return 1;  // the line's label
-  if (bit(Clo, C | QM, e - 1)) return 2;
-  return 0;
-}
-
 // Carry-in at a segment start P from the masks of the 64 bytes before it
 // (bit i <-> P-64+i), when no chunk starts in (P-64, P] and the previous run
 // and its gap lie inside those 64 bytes (the common case).  Returns false
@@ -653,11 +602,8 @@ DA_HD SegOut segment_roles(const Tile &t, int tid) {
     if (cq && (P + 64 >= a.n || t.is_cs(P + 64))) o.bad = 1;
     Q = RS & t3 & ~L;
     if (Q & K) o.bad = 1;  // a ':' and a token in one gap ("l : qid:5" pairs l with 5)
-    for (uint64_t m = Q; m; m &= m - 1) {
-      const uint32_t qb = (uint32_t)ctz64(m);
-      const int h = qid_head_planes(t, tid, P, qb, D, N, C, QM, S, F);
-      if (h == 0 || (h == 2 && !t.qid_ok(P + qb))) o.bad = 1;
-    }
+    for (uint64_t m = Q; m; m &= m - 1)
+      if (!t.qid_ok(P + ctz64(m))) o.bad = 1;
   }
   const uint64_t Z = ~RS;
   const uint64_t xl = L << 1, xk = K << 1, xq = Q << 1;

@@ -743,6 +743,7 @@ class HipTextParser : public dmlc::Parser<IndexType, DType> {
     }
     if (st) hip_check(hipEventRecord(w->ev[3], s), "hipEventRecord");
     if (again) hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
+    else if (st) hip_check(hipEventSynchronize(w->ev[3]), "hipEventSynchronize");
     const Clock clk;
     BuildBlocks(b, nunits, upc);
     if (st) {

@@ -68,6 +68,13 @@ int main(int argc, char **argv) {
       if (dm != rd || nl != rn) {
         if (bad++ < 10) printf("seg_masks mismatch off %u len %d\n", off, len);
       }
+      const uint32_t delim = "\n,;| \t:\xff"[rnd() % 8] & 0xFFu;
+      uint32_t cn, cd, rd2 = 0;
+      seg_masks_csv(win, off, len, delim, &cn, &cd);
+      for (int i = 0; i < len; ++i) rd2 |= (uint32_t)(win[off + i] == delim) << i;
+      if (cn != rn || cd != rd2) {
+        if (bad++ < 10) printf("seg_masks_csv mismatch off %u len %d delim %u\n", off, len, delim);
+      }
     }
   }
   for (long it = 0; it < n; ++it) {
