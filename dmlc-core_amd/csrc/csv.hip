@@ -10,7 +10,10 @@ namespace dmlc_amd {
 namespace {
 
 template <int MODE>
-__global__ void __launch_bounds__(kThreads) csv_tile(CsvArgs a) {
+#ifndef FEX_MINW
+#define FEX_MINW 4  // waves per SIMD the exact tile kernels are register-budgeted for (round 4: 1 -> 4, config 2 exact 13.2 -> 11.9 ms)
+#endif
+__global__ void __launch_bounds__(kThreads, FEX_MINW) csv_tile(CsvArgs a) {
   __shared__ __attribute__((aligned(16))) csv::Shared sh;
   __shared__ uint64_t scratch[kBlockScratchU64];
   DevBlock bk{scratch};

@@ -464,7 +464,11 @@ DA_HDF void tile(const LibsvmArgs &a, Shared &sh, BK &bk, uint64_t k) {
     // ---- head sections -> R1 marks, and the segment's row / weight / qid
     // counts (libsvm_parser.h:99-132)
     uint32_t hrow = 0, hw = 0, hq = 0;
+#ifdef FSVM_ABL_EX_NOHEADS  // timing ablation only
+    if (false) {
+#else
     if (sg.ls && !from_rec) {
+#endif
       uint32_t m = sg.ls;
       int chunk = sg.chunk;
       while (m) {
@@ -502,7 +506,11 @@ DA_HDF void tile(const LibsvmArgs &a, Shared &sh, BK &bk, uint64_t k) {
     } else {
       uint32_t fn = kIdentityFn;
       Roles R;
+#ifdef FSVM_ABL_EX_NOWALK  // timing ablation only
+      if (false) walk_roles(a, src, sh.r1bits, w0, sg, fn, R);
+#else
       if (sg.lo < sg.hi) walk_roles(a, src, sh.r1bits, w0, sg, fn, R);
+#endif
       else
         for (int s2 = 0; s2 < 4; ++s2) R.idx[s2] = R.val[s2] = R.dng[s2] = 0;
       uint32_t fn_total;
@@ -540,7 +548,9 @@ DA_HDF void tile(const LibsvmArgs &a, Shared &sh, BK &bk, uint64_t k) {
       if (sg.lo < sg.hi) {
         Base64 b;
         for (int i = 0; i < C_N; ++i) b.c[i] = tbase.c[i] + tot.c[i] + ex.c[i];
+#ifndef FSVM_ABL_EX_NOEMIT  // timing ablation only (tools/build_variants.sh), never shipped
         emit(a, src, sg, I, V, Dg, b, dtp);
+#endif
       }
       tot = CntAdd()(tot, wtot);
     }
