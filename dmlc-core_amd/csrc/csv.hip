@@ -11,7 +11,7 @@ namespace {
 
 template <int MODE>
 #ifndef FEX_MINW
-#define FEX_MINW 4  // waves per SIMD the exact tile kernels are register-budgeted for (round 4: 1 -> 4, config 2 exact 13.2 -> 11.9 ms)
+#define FEX_MINW 4  // waves per SIMD the exact tile kernels are register-budgeted for (round 4: 1 -> 4, config 3 exact 15.0 -> 13.6 ms; 5 waves spill more and lose: 14.9 ms)
 #endif
 __global__ void __launch_bounds__(kThreads, FEX_MINW) csv_tile(CsvArgs a) {
   __shared__ __attribute__((aligned(16))) csv::Shared sh;

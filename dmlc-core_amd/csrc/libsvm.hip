@@ -18,7 +18,7 @@ namespace {
 
 template <int MODE>
 #ifndef FEX_MINW
-#define FEX_MINW 4  // waves per SIMD the exact tile kernels are register-budgeted for (round 4: 1 -> 4, config 2 exact 13.2 -> 11.9 ms)
+#define FEX_MINW 5  // waves per SIMD the exact tile kernels are register-budgeted for (round 4: 1 -> 4 -> 5, config 2 exact 13.2 -> 11.9 -> 10.9 ms)
 #endif
 __global__ void __launch_bounds__(kThreads, FEX_MINW) libsvm_tile(LibsvmArgs a) {
   __shared__ __attribute__((aligned(16))) svm::Shared sh;
