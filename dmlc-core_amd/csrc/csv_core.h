@@ -378,7 +378,15 @@ DA_HDF void tile(const CsvArgs &a, Shared &sh, BK &bk, uint64_t k) {
     if (wend == w0) break;
     const uint64_t abase = w0 & ~15ull;
     const uint64_t nunits = (wend - abase + 15) >> 4;
-    stage_window(a.text, a.n, abase, nunits, sh.win, tid, kThreads);
+    for (uint64_t u = tid; u < nunits; u += kThreads) {
+      const uint64_t g = abase + (u << 4);
+      if (g + 16 <= a.n) {
+        for (int q = 0; q < 4; ++q)
+          reinterpret_cast<uint32_t *>(&sh.win[u << 4])[q] = reinterpret_cast<const uint32_t *>(a.text + g)[q];
+      } else {
+        for (int q = 0; q < 16; ++q) sh.win[(u << 4) + q] = g + q < a.n ? a.text[g + q] : 0;
+      }
+    }
     bk.sync();
     src.wbase = abase;
     src.wend = mn(abase + (nunits << 4), a.n);

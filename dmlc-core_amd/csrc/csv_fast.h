@@ -53,7 +53,7 @@ struct Shared {  // LDS of one workgroup
     uint32_t lst[kListCap];
   } u;
   uint32_t cls[kClsEntries];  // byte classes: byte 0 number char, 1 digit (without 0: outside the grammar),
-                              // 2 newline, 3 delimiter; bytes >= 0x80 read into dt / gw (fast_common.h)
+                              // 2 newline, 3 delimiter
   DecTables dt;
   uint32_t gw[2 * kFThreads + 2];  // digit plane as words: 2t, 2t+1 segment t; 2 kFThreads: the post-halo
   uint64_t segc;      // the tile's segmented carry (delimiters since the last row start before it)
@@ -293,23 +293,6 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
   uint64_t J = 0;  // junk bytes of my segment (JK)
   {
     Masks m = classify64_lut(sh.c.text + kPre + tid * kSegB, sh.cls);
-    if (m.hi) {  // bytes >= 0x80 (rare): their classes byte by byte (junk, a delimiter, or outside)
-      const uint8_t *seg = sh.c.text + kPre + tid * kSegB;
-      const uint64_t h = hi_mask64(seg);
-      m = classify64_lut<true>(seg, sh.cls);
-      m.d &= ~h;
-      m.g &= ~h;
-      m.n &= ~h;
-      m.c &= ~h;
-      for (uint64_t mm = h; mm; mm &= mm - 1) {
-        const uint64_t bit = mm & (0 - mm);
-        const uint32_t cb = class_of_csv(seg[ctz64(mm)], a.delim, !SP, JK);
-        if (cb & 1u) m.d |= bit;
-        if ((cb >> 8) & 1u) m.g |= bit;
-        if ((cb >> 16) & 1u) m.n |= bit;
-        if ((cb >> 24) & 1u) m.c |= bit;
-      }
-    }
     if (JK) {  // split the junk class (digit + newline) off the planes
       J = m.g & m.n;
       m.g &= ~J;

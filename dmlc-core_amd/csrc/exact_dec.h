@@ -102,36 +102,6 @@ DA_HD bool csv_value_at(const Src &src, uint64_t x, const fast::DecTables *dt, f
   return true;
 }
 
-// Stage the window [abase, abase + 16 nunits) of the text into LDS: every
-// thread issues the loads of all its 16-byte units (at most three: nunits <=
-// kWin / 16 + 1) before the first LDS store, so one HBM round trip is waited
-// for instead of one per unit.  Units past the text end are zero-filled.
-DA_HD void stage_window(const uint8_t *text, uint64_t n, uint64_t abase, uint64_t nunits, uint8_t *win, int tid,
-                        int nthreads) {
-  uint32_t v[3][4];
-  bool full[3];
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    const uint64_t u = (uint64_t)tid + (uint64_t)k * nthreads, g = abase + (u << 4);
-    full[k] = u < nunits && g + 16 <= n;
-    if (full[k])
-      for (int q = 0; q < 4; ++q) v[k][q] = reinterpret_cast<const uint32_t *>(text + g)[q];
-  }
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    const uint64_t u = (uint64_t)tid + (uint64_t)k * nthreads, g = abase + (u << 4);
-    if (full[k]) {
-      for (int q = 0; q < 4; ++q) reinterpret_cast<uint32_t *>(win + (u << 4))[q] = v[k][q];
-    } else if (u < nunits) {
-      for (int q = 0; q < 16; ++q) win[(u << 4) + q] = g + q < n ? text[g + q] : 0;
-    }
-  }
-  for (uint64_t u = (uint64_t)tid + 3ull * nthreads; u < nunits; u += nthreads) {  // (larger windows only)
-    const uint64_t g = abase + (u << 4);
-    for (int q = 0; q < 16; ++q) win[(u << 4) + q] = g + q < n ? text[g + q] : 0;
-  }
-}
-
 // Digitchar (strtonum.h:70-72) and newline masks of the len <= 32 staged
 // bytes at win + off: nine aligned LDS words funnel-shifted to the segment,
 // classified four bytes at a time by the nibble tables (fast_common.h

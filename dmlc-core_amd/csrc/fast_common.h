@@ -76,13 +76,13 @@ struct Masks {
   uint32_t hi;  // table form: a byte >= 0x80 among the 64 (its planes are not the table's)
 };
 
-// The class tables hold the 128 ASCII bytes (512 bytes of LDS per tile); a
-// byte >= 0x80 still indexes by its value -- on the device the read lands in
-// the tile's next LDS arrays (the Shared layouts put DecTables there), and its
-// planes are replaced afterwards (Masks.hi, hi_mask64): the index stays one
-// SDWA shift.  The emulator builds the same Shared structs and reads the same
-// words, so it sees what the device sees.
-constexpr int kClsEntries = 128;
+// The class tables hold all 256 byte values (1 KiB of LDS per tile): a byte
+// >= 0x80 has its own class (outside the grammar; CSV's junk), so the table
+// body needs no per-byte range check.  (Round 4 tried 128 entries -- 512 B
+// less LDS -- with the bytes >= 0x80 patched afterwards: the OR of the
+// words that finds them cost the libfm kernel 7 spilled VGPRs, and the
+// out-of-table reads leaked into neighbouring bytes' planes.)
+constexpr int kClsEntries = 256;
 DA_HD uint32_t cls_index(uint32_t b) { return b & 0xFFu; }
 // bit i: byte i of the 64 at p (16-byte aligned) is >= 0x80 (rare: a slow loop)
 DA_HD uint64_t hi_mask64(const uint8_t *p) {
@@ -189,26 +189,19 @@ DA_HD uint32_t class_of(uint32_t b) {
   return 0x00000100u;
 }
 
-// Masks of the 64 bytes at p (16-byte aligned) through the class table.  On
-// the device a byte >= 0x80 reads a word past the table whose bits, shifted
-// into the plane bytes, can land on the planes of the other bytes of its
-// 8-byte group: a segment with m.hi must be classified again with kAscii
-// (index & 0x7F, every entry a table class) before its planes are used.
-template <bool kAscii = false>
+// Masks of the 64 bytes at p (16-byte aligned) through the class table.
 DA_HD Masks classify64_lut(const uint8_t *p, const uint32_t *cls) {
   uint32_t acc[8];
-  uint32_t orv = 0;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     uint32_t w[4];
     load16(p + 16 * q, w);
-    orv |= w[0] | w[1] | w[2] | w[3];
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int b = 0; b < 4; ++b) {
         const int i = 16 * q + 4 * j + b;
-        const uint32_t x = cls[kAscii ? (w[j] >> (8 * b)) & 0x7Fu : cls_index((w[j] >> (8 * b)) & 0xFFu)];
+        const uint32_t x = cls[cls_index((w[j] >> (8 * b)) & 0xFFu)];
         if ((i & 7) == 0) acc[i >> 3] = x;
         else acc[i >> 3] |= x << (i & 7);
       }
@@ -232,8 +225,8 @@ DA_HD Masks classify64_lut(const uint8_t *p, const uint32_t *cls) {
   m.c = pc[0] | ((uint64_t)pc[1] << 32);
   const uint64_t g = pg[0] | ((uint64_t)pg[1] << 32);
   m.g = g;
-  m.hi = (orv & 0x80808080u) != 0u;
-  m.bad = (g & ~m.d) != 0 || m.hi;
+  m.hi = 0u;  // (the table classes bytes >= 0x80 itself)
+  m.bad = (g & ~m.d) != 0;
   return m;
 }
 // 4 bytes (x) through the table: 4-bit masks (a byte >= 0x80: r.hi, planes

@@ -273,7 +273,15 @@ DA_HDF void tile(const LibfmArgs &a, svm::Shared &sh, BK &bk, uint64_t k) {
     if (tid == 0) sh.pending[j & 1] = (pend != kNone && pend >= wend) ? pend : kNone;
     const uint64_t abase = w0 & ~15ull;
     const uint64_t nunits = (wend - abase + 15) >> 4;
-    stage_window(a.text, a.n, abase, nunits, sh.win, tid, kThreads);
+    for (uint64_t u = tid; u < nunits; u += kThreads) {
+      const uint64_t g = abase + (u << 4);
+      if (g + 16 <= a.n) {
+        for (int q = 0; q < 4; ++q)
+          reinterpret_cast<uint32_t *>(&sh.win[u << 4])[q] = reinterpret_cast<const uint32_t *>(a.text + g)[q];
+      } else {
+        for (int q = 0; q < 16; ++q) sh.win[(u << 4) + q] = g + q < a.n ? a.text[g + q] : 0;
+      }
+    }
     for (int i = tid; i < kWin / 32 + 1; i += kThreads) sh.r1bits[i] = 0;
     bk.sync();
     src.wbase = abase;

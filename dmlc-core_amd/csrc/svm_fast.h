@@ -140,7 +140,7 @@ constexpr uint32_t kPassRuns = (uint32_t)kListCap - kSegB;
 
 struct Shared {  // LDS of one workgroup
   TileCommon c;
-  uint32_t cls[kClsEntries];  // byte class table (fast_common.h class_of); bytes >= 0x80 read into dt / u
+  uint32_t cls[kClsEntries];  // byte class table (fast_common.h class_of)
   DecTables dt;
   union {
     Planes m;
