@@ -516,8 +516,11 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
       const uint32_t w4[4] = {(uint32_t)wq.lo, (uint32_t)(wq.lo >> 32), (uint32_t)wq.hi, (uint32_t)(wq.hi >> 32)};
       if constexpr (VT == 0) {
         v = wfloat32m(w4, M, sh.dt, &ok);
-        float x;
-        if (junk_tile && inf_nan_of(w4, &x)) v = x;
+        if (junk_tile) {  // inf / nan letters after the optional sign (rare: a branch, not a select)
+          const uint32_t b0 = w4[0] & 0xFFu, l = (b0 == '-' || b0 == '+') ? (w4[0] >> 8) & 0xFFu : b0;
+          float x;
+          if (((l | 0x20u) == 'i' || (l | 0x20u) == 'n') && inf_nan_of(w4, &x)) v = x;
+        }
       } else {
         v = wint64m(w4, M, &ok);
       }

@@ -24,11 +24,13 @@ SLOTS = 16
 def main():
     rows = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 20
     width = int(sys.argv[2]) if len(sys.argv) > 2 else 128
+    kind = {"libsvm": synth.LIBSVM, "qid": synth.LIBSVM_QID, "cmt": synth.LIBSVM_CMT}[
+        sys.argv[3] if len(sys.argv) > 3 else "libsvm"]
     dmlc_amd.LIB_PATH = os.path.join(ROOT, "dmlc-core_amd", "lib", "libdmlc_amd_stamps.so")
     L = dmlc_amd.lib()
     L.dmlc_amd_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
     import torch
-    text, _ = synth.rows(synth.LIBSVM, rows, width, seed=1)
+    text, _ = synth.rows(kind, rows, width, seed=1)
     starts = dmlc_amd.text_chunk_starts(text)
     d_text = torch.from_numpy(text).cuda()
     d_cs = torch.from_numpy(starts).cuda()
