@@ -123,14 +123,40 @@ DA_HD void seg_masks(const uint8_t *win, uint32_t off, int len, uint32_t *dm, ui
   *nl = n & m;
 }
 
-// Newline and delimiter masks of the len <= 32 staged bytes at win + off (the
-// CSV exact kernels): byte-equality by the carry-free zero-byte test on nine
-// aligned LDS words, four bytes at a time.
 DA_HD uint32_t eq_nib(uint32_t x, uint32_t rep) {  // 4 bits: byte i of x == the byte repeated in rep
   const uint32_t t = x ^ rep;
   const uint32_t nz = (((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u;  // bit 7: byte nonzero
   return ((((~nz >> 7) & 0x01010101u) * 0x01020408u) >> 24) & 0xFu;
 }
+// The same plus the ':' , blank (' ' '\t') and '#' masks: what gap_fnb
+// (libsvm_core.h) reads byte by byte, for the role walk's gap classes.
+DA_HD void seg_masks5(const uint8_t *win, uint32_t off, int len, uint32_t *dm, uint32_t *nl, uint32_t *cm,
+                      uint32_t *bm, uint32_t *hm) {
+  const uint32_t *q = reinterpret_cast<const uint32_t *>(win + (off & ~3u));
+  const uint32_t sh = 8u * (off & 3u);
+  uint32_t v[9];
+  for (int i = 0; i < 9; ++i) v[i] = q[i];
+  uint32_t d = 0, n = 0, c = 0, b = 0, h = 0;
+  for (int i = 0; i < 8; ++i) {
+    const uint32_t x = fast::funnel(v[i + 1], v[i], sh);
+    const uint32_t cls = fast::classify4(x), hi = fast::hi_nib4(x);
+    d |= (fast::nib_d(cls) & ~hi) << (4 * i);
+    n |= (fast::nib_n(cls) & ~hi) << (4 * i);
+    c |= (fast::nib_c(cls) & ~hi) << (4 * i);
+    b |= ((((((cls >> 5) | (cls >> 6)) & 0x01010101u) * 0x01020408u) >> 24) & ~hi & 0xFu) << (4 * i);
+    h |= eq_nib(x, 0x23232323u) << (4 * i);
+  }
+  const uint32_t m = len >= 32 ? ~0u : ((1u << len) - 1u);
+  *dm = d & m;
+  *nl = n & m;
+  *cm = c & m;
+  *bm = b & m;
+  *hm = h & m;
+}
+
+// Newline and delimiter masks of the len <= 32 staged bytes at win + off (the
+// CSV exact kernels): byte-equality by the carry-free zero-byte test on nine
+// aligned LDS words, four bytes at a time.
 DA_HD void seg_masks_csv(const uint8_t *win, uint32_t off, int len, uint32_t delim, uint32_t *nl, uint32_t *dl) {
   const uint32_t *q = reinterpret_cast<const uint32_t *>(win + (off & ~3u));
   const uint32_t sh = 8u * (off & 3u);

@@ -20,7 +20,10 @@ template <int MODE>
 #ifndef FEX_MINW
 #define FEX_MINW 5  // waves per SIMD the exact tile kernels are register-budgeted for (round 4: 1 -> 4 -> 5, config 2 exact 13.2 -> 11.9 -> 10.9 ms)
 #endif
-__global__ void __launch_bounds__(kThreads, FEX_MINW) libsvm_tile(LibsvmArgs a) {
+#ifndef FEX_MINW1
+#define FEX_MINW1 FEX_MINW  // the count pass's own budget
+#endif
+__global__ void __launch_bounds__(kThreads, MODE == 1 ? FEX_MINW1 : FEX_MINW) libsvm_tile(LibsvmArgs a) {
   __shared__ __attribute__((aligned(16))) svm::Shared sh;
   __shared__ uint64_t scratch[kBlockScratchU64];
   DevBlock bk{scratch};

@@ -116,6 +116,10 @@ struct Shared {  // LDS of one workgroup
 struct Seg {
   uint64_t lo, hi;      // [lo, hi) absolute
   uint32_t rs, ls, le;  // run-start / line-start / line-end masks (bit i <-> lo + i)
+  // run starts whose gap's first non-blank byte (gap_fnb) is ':' / '#', from
+  // the segment's masks; xg: the first run start when no digitchar precedes
+  // it in the segment -- its gap may begin before it (gap_fnb reads that one)
+  uint32_t rc, rh, xg;
   int chunk;            // chunk of position lo
 };
 
@@ -167,7 +171,8 @@ DA_HDF void walk_roles(const LibsvmArgs &a, Src &src, const uint32_t *r1bits, ui
         fn = 0x55u;  // every entry -> FIRST, the run an index
         for (int s = 0; s < 4; ++s) R.idx[s] |= bit;
       } else if ((fn ^ (fn >> 1)) & 0x55u) {  // some entry is F or S
-        const uint32_t g = gap_fnb(src, x, cfloor);
+        const uint32_t g = (sg.xg & bit) ? gap_fnb(src, x, cfloor)
+                           : (sg.rc & bit) ? (uint32_t)':' : (sg.rh & bit) ? (uint32_t)'#' : 0u;
         const uint32_t tF = g == '#' ? S_D : (g == ':' ? S_S : S_F);
         const uint32_t tS = g == '#' ? S_D : S_F;
         for (int s = 0; s < 4; ++s) {
@@ -439,19 +444,30 @@ DA_HDF void tile(const LibsvmArgs &a, Shared &sh, BK &bk, uint64_t k) {
     Seg sg;
     sg.lo = w0 + (uint64_t)tid * kSeg;
     sg.hi = mn(sg.lo + (uint64_t)kSeg, wend);
-    sg.rs = sg.ls = sg.le = 0;
+    sg.rs = sg.ls = sg.le = sg.rc = sg.rh = sg.xg = 0;
     sg.chunk = 0;
     if (sg.lo < sg.hi) {
       sg.chunk = chunk_of(a.cs, a.nchunk, sg.lo);
       src.lim = a.lim(sg.chunk);
-      uint32_t dm, nl, csm = 0;
+      uint32_t dm, nl, cm, bm, hm, csm = 0;
       const int len = (int)(sg.hi - sg.lo);
-      seg_masks(sh.win, (uint32_t)(sg.lo - abase), len, &dm, &nl);
+      seg_masks5(sh.win, (uint32_t)(sg.lo - abase), len, &dm, &nl, &cm, &bm, &hm);
       for (int c = sg.chunk; c < a.nchunk && a.cs[c] < sg.hi; ++c)
         if (a.cs[c] >= sg.lo) csm |= 1u << (a.cs[c] - sg.lo);
       const uint32_t prev = (sg.lo > 0 && !(csm & 1u) && is_digitchar(src(sg.lo - 1))) ? 1u : 0u;
       sg.rs = (dm & ~((dm << 1) | prev)) | (csm & dm);
       sg.ls = nl | csm;
+      {  // gap classes: the carry from each gap start runs through its blanks to
+         // its first non-blank; a ':' / '#' there is carried on through the gap
+         // to the run start that ends it
+        const uint32_t lenm = len >= 32 ? ~0u : ((1u << len) - 1u);
+        const uint32_t G = ~dm & lenm, Bg = bm & G;
+        const uint32_t F = (Bg + (G & ~(G << 1))) & ~Bg & G;
+        sg.rc = (G + (F & cm)) & ~G & dm;
+        sg.rh = (G + (F & hm)) & ~G & dm;
+        const uint32_t rs0 = sg.rs & (0u - sg.rs);  // the first run's gap may begin before the segment
+        sg.xg = (dm & (rs0 - 1u)) == 0u ? rs0 : 0u;
+      }
       bool nxt = sg.hi == a.n;  // is position hi a line start (or the end of data)?
       if (!nxt) {
         const uint64_t h = sg.hi;

@@ -68,6 +68,18 @@ int main(int argc, char **argv) {
       if (dm != rd || nl != rn) {
         if (bad++ < 10) printf("seg_masks mismatch off %u len %d\n", off, len);
       }
+      {
+        uint32_t d5, n5, c5, b5, h5, rc = 0, rb = 0, rh = 0;
+        seg_masks5(win, off, len, &d5, &n5, &c5, &b5, &h5);
+        for (int i = 0; i < len; ++i) {
+          rc |= (uint32_t)(win[off + i] == ':') << i;
+          rb |= (uint32_t)is_blank(win[off + i]) << i;
+          rh |= (uint32_t)(win[off + i] == '#') << i;
+        }
+        if (d5 != rd || n5 != rn || c5 != rc || b5 != rb || h5 != rh) {
+          if (bad++ < 10) printf("seg_masks5 mismatch off %u len %d\n", off, len);
+        }
+      }
       const uint32_t delim = "\n,;| \t:\xff"[rnd() % 8] & 0xFFu;
       uint32_t cn, cd, rd2 = 0;
       seg_masks_csv(win, off, len, delim, &cn, &cd);

@@ -591,3 +591,37 @@ def test_emu_csv_chunk_cut_edges(vt):
         assert (o["status"] != 0) == failed, (data, offs, o["msg"], h["error"])
         if not failed:
             assert diff(h, o) == [], (data, offs, diff(h, o))
+
+
+def test_emu_exact_gaps_across_segments():
+    """The exact libsvm kernels classify each run's gap from the segment's
+    masks (libsvm_core.h Seg.rc / rh) and read the bytes only for a segment's
+    first run: ':' / '#' / blanks at every offset against the 32-byte segment
+    and 8 KiB window edges, on the exact path, equal the oracle."""
+    rng = np.random.default_rng(2024)
+    checked = 0
+    for it in range(40):
+        rows = []
+        for r in range(int(rng.integers(20, 200))):
+            parts = ["%d" % (r % 3)]
+            for j in range(int(rng.integers(0, 12))):
+                gap = " " * int(rng.integers(1, 4))
+                # (index-only runs among valued ones fail the reference's GetBlock CHECK:
+                # every 4th input has no values at all instead)
+                colon = "" if it % 4 == 3 else str(rng.choice([":", " :", ": ", " : ", "  :"],
+                                                             p=[0.7, 0.1, 0.1, 0.05, 0.05]))
+                parts.append("%s%d%s%s" % (gap, int(rng.integers(0, 999)), colon,
+                                           ("%.4g" % rng.random()) if colon else ""))
+            if rng.random() < 0.15:
+                parts.append(" # c %d:%d" % (r, r))
+            rows.append("".join(parts))
+        data = (" " * int(rng.integers(0, 33)) + "\n".join(rows) + "\n").encode()
+        offs = [0, len(data)]
+        o = po.parse_chunks(data, offs, fmt=po.LIBSVM)
+        h = pyemu.parse(data, offs, "libsvm", exact=True, tile_bytes=int(rng.choice([0, 4096, 9000])))
+        failed = check_fail(h, "libsvm", offs)
+        assert (o["status"] != 0) == failed, (it, o["msg"], h["error"])
+        if not failed:
+            assert diff(h, o) == [], (it, diff(h, o))
+        checked += not failed
+    assert checked >= 30, checked
