@@ -449,15 +449,18 @@ DA_HDF void tile(const LibsvmArgs &a, Shared &sh, BK &bk, uint64_t k) {
     if (sg.lo < sg.hi) {
       sg.chunk = chunk_of(a.cs, a.nchunk, sg.lo);
       src.lim = a.lim(sg.chunk);
-      uint32_t dm, nl, cm, bm, hm, csm = 0;
+      uint32_t dm, nl, cm = 0, bm = 0, hm = 0, csm = 0;
       const int len = (int)(sg.hi - sg.lo);
-      seg_masks5(sh.win, (uint32_t)(sg.lo - abase), len, &dm, &nl, &cm, &bm, &hm);
+      // (a window with a count-pass record walks no roles: its run starts'
+      // gap classes are not needed)
+      if (from_rec) seg_masks(sh.win, (uint32_t)(sg.lo - abase), len, &dm, &nl);
+      else seg_masks5(sh.win, (uint32_t)(sg.lo - abase), len, &dm, &nl, &cm, &bm, &hm);
       for (int c = sg.chunk; c < a.nchunk && a.cs[c] < sg.hi; ++c)
         if (a.cs[c] >= sg.lo) csm |= 1u << (a.cs[c] - sg.lo);
       const uint32_t prev = (sg.lo > 0 && !(csm & 1u) && is_digitchar(src(sg.lo - 1))) ? 1u : 0u;
       sg.rs = (dm & ~((dm << 1) | prev)) | (csm & dm);
       sg.ls = nl | csm;
-      {  // gap classes: the carry from each gap start runs through its blanks to
+      if (!from_rec) {  // gap classes: the carry from each gap start runs through its blanks to
          // its first non-blank; a ':' / '#' there is carried on through the gap
          // to the run start that ends it
         const uint32_t lenm = len >= 32 ? ~0u : ((1u << len) - 1u);
