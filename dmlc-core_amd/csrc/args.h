@@ -103,7 +103,7 @@ constexpr uint64_t kFastLbWords = 5;
 // Threads of a single-pass tile (fast_common.h): four waves, 16 KiB tiles.
 // One wave per tile (4 KiB tiles, no barriers between waves, -DFAST_THREADS=64)
 // and two (128) stay buildable for A/B timing; on MI355X they measured
-// 3.90 / 2.25 ms against 1.78 ms on config 2 (gpurun_out/ab_r4f.txt: per wave
+// 3.90 / 2.25 ms against 1.78 ms on config 2 (profiles/r4_ab/ab_r4f.txt, PMC in gpurun_out/ab: per wave
 // VALU 2725 / 1961 / 1709 -- the tile-level work of the look-back, the unit
 // search and the run-list rounds does not shrink with the tile).
 #ifndef FAST_THREADS

@@ -353,7 +353,7 @@ struct EngineConfig {
   // "h2d_kernel" / "d2h_kernel": one direction by kernel, the other by DMA
   // (the SDMA engines and the copy kernels then carry different directions).
   // Default "d2h_kernel" (round 4: 28.8-30.3 GB/s against 25.7-28.4 for
-  // "kernel" over two sweeps on config 2, gpurun_out/e2e_sweep_r4*.txt).
+  // "kernel" over two sweeps on config 2, profiles/r4_e2e_sweep_r4*.txt).
   enum CopyMode { kKernel, kDma, kH2DKernel, kD2HKernel } copy_mode = kD2HKernel;
   // DMLC_AMD_PRECOPY=0: the CSR copy-out waits for the parse's result on the
   // host (sizes exact) instead of being queued behind the parse with sizes
