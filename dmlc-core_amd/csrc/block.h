@@ -120,6 +120,38 @@ struct DevBlockT {
     return pre + inc - v;
   }
 
+  // The same with one barrier: every wave reads all wave totals itself.  The
+  // scratch slots stay read until the caller's next barrier, so a second
+  // scan must not follow before one.
+  template <typename T, typename Op>
+  __device__ __forceinline__ T exclusive1(T v, T identity, Op op, T *total) const {
+    static_assert(sizeof(T) <= kSlot, "scan element larger than the scratch slot");
+    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+    T inc = v;
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+      T o = shfl_up(inc, d);
+      if (lane >= d) inc = op(o, inc);
+    }
+    const T up = shfl_up(inc, 1);
+    if constexpr (NW == 1) {
+      *total = shfl(inc, kWave - 1);
+      return lane == 0 ? identity : up;
+    }
+    T *sc = reinterpret_cast<T *>(scratch);
+    if (lane == kWave - 1) *reinterpret_cast<T *>(reinterpret_cast<char *>(sc) + kSlot * wid) = inc;
+    __syncthreads();
+    T pre = identity, tot = identity;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      const T t = *reinterpret_cast<T *>(reinterpret_cast<char *>(sc) + kSlot * w);
+      if (w < wid) pre = op(pre, t);
+      tot = op(tot, t);
+    }
+    *total = tot;
+    return lane == 0 ? pre : op(pre, up);
+  }
+
   // Exclusive prefix (identity for thread 0) and the block total.
   template <typename T, typename Op>
   __device__ __forceinline__ T exclusive(T v, T identity, Op op, T *total) const {

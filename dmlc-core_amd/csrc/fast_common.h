@@ -13,15 +13,18 @@ namespace fast {
 // Tile geometry: kFThreads threads (args.h kFastThreads), 64 text bytes each.
 constexpr int kFThreads = kFastThreads;
 constexpr int kFWaves = kFThreads / kWave;
-static_assert(kFThreads % kWave == 0 && kFWaves >= 1 && kFWaves <= 4, "whole waves, at most four");
+static_assert(kFThreads % kWave == 0 && (kFWaves == 1 || kFWaves == 2 || kFWaves == 4 || kFWaves == 6 || kFWaves == 8),
+              "whole waves: 1, 2, 4, 6 or 8");
 
 // LDS of one single-pass workgroup.  gfx950 allocates LDS in 1280-byte
 // granules (160 KiB / 128): at four waves per tile, 6 workgroups per CU fit
 // 21 granules each (26,880 bytes), one byte more and the launch dropped to 5
 // per CU (+32 bytes took svm_fast_tile from 1.84 to 2.04 ms); a one-wave
-// tile gets 6 granules (7,680 bytes: 21 workgroups per CU).
+// tile gets 6 granules (7,680 bytes: 21 workgroups per CU); six- and eight-wave
+// tiles (24 / 32 KiB of text) get 4 and 3 workgroups per CU: 32 and 42 granules.
 constexpr int kLdsGranule = 1280;
-constexpr int kLdsBudget = (kFWaves == 1 ? 6 : kFWaves == 2 ? 11 : 21) * kLdsGranule;
+constexpr int kLdsBudget =
+    (kFWaves == 1 ? 6 : kFWaves == 2 ? 11 : kFWaves == 4 ? 21 : kFWaves == 6 ? 32 : 42) * kLdsGranule;
 
 constexpr int kSegB = 64;                 // bytes per thread (one 64-bit mask)
 constexpr int kTile = kFThreads * kSegB;  // text per tile (4 KiB at one wave)
@@ -229,6 +232,56 @@ DA_HD Masks classify64_lut(const uint8_t *p, const uint32_t *cls) {
   m.bad = (g & ~m.d) != 0;
   return m;
 }
+// ---- The same masks in registers (A/B build FSVM_REGCLS): eight one-bit
+// classes from two nibble tables by v_perm (digit, + - ., e E, ':', newline,
+// space, tab, and the letters a d i q t y, which qid_clean checks against
+// "qid:" as the table's N+C letters), then per plane a flag bit per byte
+// gathered four at a time by one multiply and shifted in by v_alignbit.
+constexpr uint32_t kRLoA = 0x01018121u, kRLoB = 0x01010581u, kRLoC = 0x0218C101u, kRLoD = 0x00021200u;
+constexpr uint32_t kRHiA = 0x09220050u, kRHiB = 0x80840004u;
+DA_HD uint32_t rcls4(uint32_t x) {  // one class bit per byte (0: outside the grammar)
+  const uint32_t s = x & 0x07070707u;
+  const uint32_t a = perm_b32(kRLoB, kRLoA, s), b = perm_b32(kRLoD, kRLoC, s);
+  const uint32_t m = perm_b32(0xFFFFFFFFu, 0u, (x >> 1) & 0x04040404u);  // 0xFF where the low nibble >= 8
+  const uint32_t hv = perm_b32(kRHiB, kRHiA, (x >> 4) & 0x07070707u);
+  return ((b & m) | (a & ~m)) & hv;
+}
+DA_HD uint32_t gather_in(uint32_t acc, uint32_t f, uint32_t mul) {  // acc << 4 | the 4 flags (one bit per byte)
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_alignbit(acc, f * mul, 28u);
+#else
+  return (acc << 4) | ((f * mul) >> 28);
+#endif
+}
+DA_HD Masks classify64_reg(const uint8_t *p) {
+  uint32_t d[2] = {0, 0}, g[2] = {0, 0}, n[2] = {0, 0}, c[2] = {0, 0};
+  uint32_t all = 0x80808080u, orv = 0;
+#pragma unroll
+  for (int q = 3; q >= 0; --q) {  // last dword first: each gather shifts the earlier ones up
+    uint32_t w[4];
+    load16(p + 16 * q, w);
+#pragma unroll
+    for (int j = 3; j >= 0; --j) {
+      const int h = q >> 1;
+      const uint32_t x = w[j], cls = rcls4(x);
+      all &= cls + 0x7F7F7F7Fu;
+      orv |= x;
+      g[h] = gather_in(g[h], cls & 0x01010101u, 0x10204080u);
+      d[h] = gather_in(d[h], ((cls & 0x07070707u) + 0x03030303u) & 0x04040404u, 0x04081020u);
+      n[h] = gather_in(n[h], ((cls & 0x90909090u) + 0x70707070u) & 0x80808080u, 0x00204081u);
+      c[h] = gather_in(c[h], ((cls & 0x88888888u) + 0x78787878u) & 0x80808080u, 0x00204081u);
+    }
+  }
+  Masks m;
+  m.d = d[0] | ((uint64_t)d[1] << 32);
+  m.g = g[0] | ((uint64_t)g[1] << 32);
+  m.n = n[0] | ((uint64_t)n[1] << 32);
+  m.c = c[0] | ((uint64_t)c[1] << 32);
+  m.hi = 0u;
+  m.bad = ((all & 0x80808080u) != 0x80808080u) || (orv & 0x80808080u);
+  return m;
+}
+
 // 4 bytes (x) through the table: 4-bit masks (a byte >= 0x80: r.hi, planes
 // cleared, bad; its table word is masked to the plane bits so that it cannot
 // reach the other bytes' planes)
@@ -557,6 +610,28 @@ DA_HD W16 win_at_o(const uint8_t *text, uint32_t o) {
   q.lo = v.x | ((uint64_t)v.y << 32);
   q.hi = v.z | ((uint64_t)v.w << 32);
   return q;
+#endif
+#if defined(FSVM_WIN64)
+  {  // three 8-byte aligned reads (a wave's windows are ~16 B apart: b32 reads 4-way conflict)
+    const uint32_t off = o + kPre;
+    // (each address made opaque: merged into ds_read2_b64 the pair costs twice two ds_read_b64)
+    uint32_t a0 = off & ~7u, a1 = a0 + 8u, a2 = a0 + 16u;
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" : "+v"(a1));
+    asm volatile("" : "+v"(a2));
+#endif
+    const uint64_t a = *reinterpret_cast<const uint64_t *>(text + a0), b = *reinterpret_cast<const uint64_t *>(text + a1),
+                   c = *reinterpret_cast<const uint64_t *>(text + a2);
+    const bool s = (off & 4u) != 0u;
+    const uint32_t x0 = s ? (uint32_t)(a >> 32) : (uint32_t)a, x1 = s ? (uint32_t)b : (uint32_t)(a >> 32),
+                   x2 = s ? (uint32_t)(b >> 32) : (uint32_t)b, x3 = s ? (uint32_t)c : (uint32_t)(b >> 32),
+                   x4 = s ? (uint32_t)(c >> 32) : (uint32_t)c;
+    const uint32_t sft = (off & 3u) * 8u;
+    W16 r;
+    r.lo = funnel(x1, x0, sft) | ((uint64_t)funnel(x2, x1, sft) << 32);
+    r.hi = funnel(x3, x2, sft) | ((uint64_t)funnel(x4, x3, sft) << 32);
+    return r;
+  }
 #endif
   const uint32_t off = o + kPre;
   const uint32_t *w = reinterpret_cast<const uint32_t *>(text + (off & ~3u));
