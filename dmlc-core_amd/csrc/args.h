@@ -50,6 +50,10 @@ struct LibsvmArgs {
   uint32_t *rec;
   uint64_t *rec_meta;
   uint32_t rec_win;  // windows per tile with a record (the rest: worked out again)
+  // count pass after the single-pass kernel (libsvm.hip libsvm_tile): its qid
+  // shards and result block, to hand a qid / no-qid mix over (NULL: no check)
+  const uint64_t *qsum;
+  const uint64_t *qres;
 };
 // windows per exact tile with a count-pass record, and the record bytes
 // (libsvm_core.h); the records are kept only while they stay within about
@@ -87,7 +91,8 @@ struct FastSvmArgs {
   uint64_t cap[8];
   uint64_t *chunk_tab;  // may be null
   uint64_t *lb;         // look-back records [5 ntiles] (status words zeroed per launch)
-  uint64_t *qsum;       // libsvm: qid runs, sharded by tile [kLabShards][8] (zeroed per launch)
+  uint64_t *qsum;       // libsvm: qid runs, sharded by tile [kLabShards][8] (zeroed per launch);
+                        // word 1 of shard 0: some tile held a qid run
   uint64_t *umin;       // indexing_mode < 0: minimum stored index (libfm: and field) per ParseBlock
                         // unit [nchunk], ~0 = none; filled by the write pass (svm_fast.h umin_fix)
   uint32_t *gate;       // != 0: input left the grammar -> exact path

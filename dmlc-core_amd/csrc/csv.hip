@@ -73,12 +73,6 @@ __global__ void label_check_kernel(const uint64_t *labsum, uint32_t *gate) {
   if (i == 0 && (a != 0 || b != 0 || c != 0)) *gate |= 1u;
 }
 
-// the error of whichever path produced the result
-__global__ void select_kernel(uint64_t *res, const uint32_t *gate, const unsigned long long *ferr) {
-  if (*gate == 0) res[8] = *ferr;
-  if (res[8] == ~0ull) res[8] = 0;
-  res[9] = *gate;  // dmlc_amd_result.path
-}
 
 }  // namespace
 
@@ -86,23 +80,23 @@ hipError_t launch_csv(const CsvArgs &a, const FastCsvArgs &f, bool use_fast, uin
                       hipStream_t s) {
   hipError_t e;
   uint32_t *gate = f.gate;
+  // ---- set-up, one launch (libsvm.hip launch_libsvm)
+  FillList fl{};
   if (phase != kPhaseFill) {
-    if ((e = hipMemsetAsync(res, 0, 16 * sizeof(uint64_t), s)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(res + 8, 0xFF, sizeof(uint64_t), s)) != hipSuccess) return e;
-    if ((e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(gate), use_fast ? 0 : 1, 1, s)) !=
-        hipSuccess)
-      return e;
+    fill_result(fl, res);
+    fl.gate = gate;
+    fl.gate_v = use_fast ? 0u : 1u;
   }
-  if (phase != kPhaseCount && f.chunk_tab &&
-      (e = hipMemsetAsync(f.chunk_tab, 0xFF, (size_t)f.nchunk * 8 * sizeof(uint64_t), s)) != hipSuccess)
-    return e;  // rows no tile writes are filled by chunk_fixup_kernel
+  if (phase != kPhaseCount) fl.add(f.chunk_tab, (uint64_t)f.nchunk * 8, ~0ull);  // rows no tile writes: finish kernel
+  fl.add(reinterpret_cast<uint64_t *>(f.err), 1, ~0ull);
+  const bool sp = f.label_col >= 0 || f.weight_col >= 0;
   if (use_fast) {
-    if ((e = hipMemsetAsync(f.err, 0xFF, sizeof(uint64_t), s)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(f.lb, 0, (size_t)f.ntiles * 8 * sizeof(uint64_t), s)) != hipSuccess) return e;
-    if ((f.label_col >= 0 || f.weight_col >= 0) &&
-        (e = hipMemsetAsync(f.labsum, 0, kLabShards * 8 * sizeof(uint64_t), s)) != hipSuccess)
-      return e;
-    const bool sp = f.label_col >= 0 || f.weight_col >= 0;
+    fl.add(f.lb, (uint64_t)f.ntiles * 8, 0);
+    if (sp) fl.add(f.labsum, kLabShards * 8, 0);
+  }
+  if (!a.ntiles && phase != kPhaseCount) fl.add(reinterpret_cast<uint64_t *>(a.offset), 1, 0);  // empty input: offset = {0}
+  if ((e = launch_prologue(fl, s)) != hipSuccess) return e;
+  if (use_fast) {
     const bool iv = f.vtype != 0;
     if (phase == kPhaseCount) {
       prof_mark(0, s, iv ? "csv_fast_tile_int<1>" : "csv_fast_tile<1>");
@@ -117,19 +111,18 @@ hipError_t launch_csv(const CsvArgs &a, const FastCsvArgs &f, bool use_fast, uin
       else csv_fast_tile<2><<<f.ntiles, fast::kFThreads, 0, s>>>(f);
       prof_mark(1, s, "csv_fast_tile<2>");
     }
-    if (f.label_col >= 0 || f.weight_col >= 0) label_check_kernel<<<1, kLabShards, 0, s>>>(f.labsum, gate);
-  } else if ((e = hipMemsetAsync(f.err, 0xFF, sizeof(uint64_t), s)) != hipSuccess) {
-    return e;
+    if (sp) label_check_kernel<<<1, kLabShards, 0, s>>>(f.labsum, gate);
   }
   // ---- exact path, gated on the device flag (early exit when the fast path stood)
   if (phase == kPhaseFill) reopen_kernel<<<1, 1, 0, s>>>(res, a.offset, a.cap[C_ROWS], gate);
-  if (!a.ntiles && phase != kPhaseCount && a.offset && (e = hipMemsetAsync(a.offset, 0, 8, s)) != hipSuccess)
-    return e;  // empty input: offset = {0}
+  const bool reset_tab = use_fast && phase != kPhaseCount && f.chunk_tab && f.nchunk > 0;
+  uint64_t *rtab = reset_tab ? f.chunk_tab : nullptr;
+  const uint64_t ntab = reset_tab ? (uint64_t)f.nchunk * 8 : 0;
   if (a.ntiles) {
     if (phase != kPhaseFill) {
       csv_tile<1><<<a.ntiles, kThreads, 0, s>>>(a);
       tile_scan_kernel<<<1, kThreads, 0, s>>>(a.tile_cnt, const_cast<uint64_t *>(a.tile_base), a.ntiles,
-                                              res, a.offset, a.cap[C_ROWS], gate);
+                                              res, a.offset, a.cap[C_ROWS], gate, rtab, ntab, gate);
       if (phase == kPhaseCount) note_gate_kernel<<<1, 1, 0, s>>>(gate);
     } else {
       // the count phase stood on the single-pass kernel but its write pass
@@ -139,18 +132,15 @@ hipError_t launch_csv(const CsvArgs &a, const FastCsvArgs &f, bool use_fast, uin
       ra.gate = gate + 2;
       csv_tile<1><<<a.ntiles, kThreads, 0, s>>>(ra);
       tile_scan_kernel<<<1, kThreads, 0, s>>>(a.tile_cnt, const_cast<uint64_t *>(a.tile_base), a.ntiles,
-                                              res, a.offset, a.cap[C_ROWS], gate + 2);
+                                              res, a.offset, a.cap[C_ROWS], gate + 2, rtab, ntab, gate);
     }
     if (phase != kPhaseCount) {
-      if (use_fast && f.chunk_tab && f.nchunk > 0)
-        tab_reset_kernel<<<(f.nchunk * 8 + 255) / 256, 256, 0, s>>>(f.chunk_tab, (uint64_t)f.nchunk * 8, gate);
       if (!use_fast) prof_mark(0, s, "csv_tile<2>");
       csv_tile<2><<<a.ntiles, kThreads, 0, s>>>(a);
       if (!use_fast) prof_mark(1, s, "csv_tile<2>");
     }
   }
-  select_kernel<<<1, 1, 0, s>>>(res, gate, f.err);
-  if (phase != kPhaseCount && f.chunk_tab && f.nchunk > 0) chunk_fixup_kernel<<<1, 256, 0, s>>>(f.chunk_tab, f.nchunk, res);
+  finish_kernel<<<1, 256, 0, s>>>(res, gate, f.err, phase != kPhaseCount ? f.chunk_tab : nullptr, f.nchunk);
   return hipGetLastError();
 }
 

@@ -46,12 +46,6 @@ __global__ void fm_reopen_kernel(uint64_t *res, uint64_t *offset, uint64_t cap_r
   if (offset && res[0] < cap_rows + 1) offset[res[0]] = res[1];
 }
 
-// the error of whichever path produced the result
-__global__ void fm_select_kernel(uint64_t *res, const uint32_t *gate, const unsigned long long *ferr) {
-  if (*gate == 0) res[8] = *ferr;
-  if (res[8] == ~0ull) res[8] = 0;
-  res[9] = *gate;  // dmlc_amd_result.path
-}
 
 }  // namespace
 
@@ -59,47 +53,41 @@ hipError_t launch_libfm(const LibfmArgs &a, const FastSvmArgs &f, bool use_fast,
                         hipStream_t s) {
   hipError_t e;
   uint32_t *gate = f.gate;
+  // ---- set-up, one launch (libsvm.hip launch_libsvm)
+  FillList fl{};
   if (phase != kPhaseFill) {
-    if ((e = hipMemsetAsync(res, 0, 16 * sizeof(uint64_t), s)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(res + 8, 0xFF, sizeof(uint64_t), s)) != hipSuccess) return e;
-    if ((e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(gate), use_fast ? 0 : 1, 1, s)) !=
-        hipSuccess)
-      return e;
+    fill_result(fl, res);
+    fl.gate = gate;
+    fl.gate_v = use_fast ? 0u : 1u;
   }
-  if (phase != kPhaseCount && a.chunk_tab &&
-      (e = hipMemsetAsync(a.chunk_tab, 0xFF, (size_t)a.nchunk * 8 * sizeof(uint64_t), s)) != hipSuccess)
-    return e;  // rows no tile writes are filled by chunk_fixup_kernel
+  if (phase != kPhaseCount) fl.add(a.chunk_tab, (uint64_t)a.nchunk * 8, ~0ull);  // rows no tile writes: finish kernel
+  fl.add(reinterpret_cast<uint64_t *>(f.err), 1, ~0ull);
   if (use_fast) {
-    if ((e = hipMemsetAsync(f.err, 0xFF, sizeof(uint64_t), s)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(f.lb, 0, (size_t)f.ntiles * fast::kLbWords * sizeof(uint64_t), s)) != hipSuccess) return e;
+    fl.add(f.lb, (uint64_t)f.ntiles * fast::kLbWords, 0);
+    if (phase != kPhaseCount && f.indexing_mode < 0) fl.add(f.umin, (uint64_t)f.nchunk, ~0ull);
+  }
+  if (phase != kPhaseFill && a.indexing_mode < 0) fl.add(a.chunk_min, (uint64_t)a.nchunk, ~0ull);
+  if (!a.ntiles && phase != kPhaseCount) fl.add(a.offset, 1, 0);  // empty input: offset = {0}
+  if ((e = launch_prologue(fl, s)) != hipSuccess) return e;
+  if (use_fast) {
     if (phase == kPhaseCount) {
       fm_fast_tile<1><<<f.ntiles, fast::kFThreads, 0, s>>>(f);
     } else {
-      if (f.indexing_mode < 0 &&
-          (e = hipMemsetAsync(f.umin, 0xFF, (size_t)f.nchunk * sizeof(uint64_t), s)) != hipSuccess)
-        return e;
       prof_mark(0, s, "fm_fast_tile<2>");
       fm_fast_tile<2><<<f.ntiles, fast::kFThreads, 0, s>>>(f);
       prof_mark(1, s, "fm_fast_tile<2>");
     }
-  } else if ((e = hipMemsetAsync(f.err, 0xFF, sizeof(uint64_t), s)) != hipSuccess) {
-    return e;
   }
   // ---- exact path, gated on the device flag (early exit when the fast path stood)
-  if (phase != kPhaseFill) {
-    if (a.indexing_mode < 0 &&
-        (e = hipMemsetAsync(a.chunk_min, 0xFF, (size_t)a.nchunk * sizeof(uint64_t), s)) != hipSuccess)
-      return e;
-  } else {
-    fm_reopen_kernel<<<1, 1, 0, s>>>(res, a.offset, a.cap[C_ROWS], gate);
-  }
-  if (!a.ntiles && phase != kPhaseCount && a.offset && (e = hipMemsetAsync(a.offset, 0, 8, s)) != hipSuccess)
-    return e;  // empty input: offset = {0}
+  if (phase == kPhaseFill) fm_reopen_kernel<<<1, 1, 0, s>>>(res, a.offset, a.cap[C_ROWS], gate);
+  const bool reset_tab = use_fast && phase != kPhaseCount && a.chunk_tab && f.nchunk > 0;
+  uint64_t *rtab = reset_tab ? a.chunk_tab : nullptr;
+  const uint64_t ntab = reset_tab ? (uint64_t)f.nchunk * 8 : 0;
   if (a.ntiles) {
     if (phase != kPhaseFill) {
       libfm_tile<1><<<a.ntiles, kThreads, 0, s>>>(a);
       tile_scan_kernel<<<1, kThreads, 0, s>>>(a.tile_cnt, const_cast<uint64_t *>(a.tile_base), a.ntiles,
-                                              res, a.offset, a.cap[C_ROWS], gate);
+                                              res, a.offset, a.cap[C_ROWS], gate, rtab, ntab, gate);
       if (phase == kPhaseCount) note_gate_kernel<<<1, 1, 0, s>>>(gate);
     } else {
       // the count phase stood on the single-pass kernel but its write pass
@@ -109,18 +97,15 @@ hipError_t launch_libfm(const LibfmArgs &a, const FastSvmArgs &f, bool use_fast,
       ra.gate = gate + 2;
       libfm_tile<1><<<a.ntiles, kThreads, 0, s>>>(ra);
       tile_scan_kernel<<<1, kThreads, 0, s>>>(a.tile_cnt, const_cast<uint64_t *>(a.tile_base), a.ntiles,
-                                              res, a.offset, a.cap[C_ROWS], gate + 2);
+                                              res, a.offset, a.cap[C_ROWS], gate + 2, rtab, ntab, gate);
     }
     if (phase != kPhaseCount) {
-      if (use_fast && a.chunk_tab && f.nchunk > 0)
-        tab_reset_kernel<<<(f.nchunk * 8 + 255) / 256, 256, 0, s>>>(a.chunk_tab, (uint64_t)f.nchunk * 8, gate);
       if (!use_fast) prof_mark(0, s, "libfm_tile<2>");
       libfm_tile<2><<<a.ntiles, kThreads, 0, s>>>(a);
       if (!use_fast) prof_mark(1, s, "libfm_tile<2>");
     }
   }
-  fm_select_kernel<<<1, 1, 0, s>>>(res, gate, f.err);
-  if (phase != kPhaseCount && a.chunk_tab && a.nchunk > 0) chunk_fixup_kernel<<<1, 256, 0, s>>>(a.chunk_tab, a.nchunk, res);
+  finish_kernel<<<1, 256, 0, s>>>(res, gate, f.err, phase != kPhaseCount ? a.chunk_tab : nullptr, a.nchunk);
   if (use_fast && phase != kPhaseCount && f.indexing_mode < 0 &&
       (e = launch_umin_fix(f.index, f.field, f.wide, f.chunk_tab, f.nchunk, f.umin, res, gate, f.cap[C_INDEX], f.cap[C_FIELD], s)) !=
           hipSuccess)

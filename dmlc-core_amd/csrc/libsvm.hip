@@ -27,6 +27,22 @@ __global__ void __launch_bounds__(kThreads, MODE == 1 ? FEX_MINW1 : FEX_MINW) li
   __shared__ __attribute__((aligned(16))) svm::Shared sh;
   __shared__ uint64_t scratch[kBlockScratchU64];
   DevBlock bk{scratch};
+  if (MODE == 1 && a.qsum && *a.gate == 0) {  // block-uniform
+    // the single pass stood; its qid runs stand only when every row has one
+    // (svm_fast.h qid_decide): a mix of rows with and without a qid hands the
+    // input over here, a clean qid input is finished by finish_kernel
+    if (a.qsum[1] == 0) return;  // no tile held a qid run
+    __shared__ int mix;
+    if (threadIdx.x < kWave) {
+      uint64_t t = a.qsum[threadIdx.x * 8];
+      for (int d = 32; d >= 1; d >>= 1) t += __shfl_xor(t, d, kWave);
+      if (threadIdx.x == 0) mix = t != a.qres[C_ROWS];
+    }
+    __syncthreads();
+    if (!mix) return;
+    if (threadIdx.x == 0) atomic_or_u32(const_cast<uint32_t *>(a.gate), 1u);
+    a.gate = nullptr;
+  }
   svm::tile<MODE>(a, sh, bk, blockIdx.x);
 }
 
@@ -120,12 +136,6 @@ __global__ void __launch_bounds__(256) qid_fix_kernel(const uint64_t *qsum, uint
     }
 }
 
-// the error of whichever path produced the result
-__global__ void select_kernel(uint64_t *res, const uint32_t *gate, const unsigned long long *ferr) {
-  if (*gate == 0) res[8] = *ferr;
-  if (res[8] == ~0ull) res[8] = 0;
-  res[9] = *gate;  // dmlc_amd_result.path
-}
 
 }  // namespace
 
@@ -133,53 +143,57 @@ hipError_t launch_libsvm(const LibsvmArgs &a, const FastSvmArgs &f, bool use_fas
                          int phase, hipStream_t s) {
   hipError_t e;
   uint32_t *gate = f.gate;
+  // ---- set-up, one launch: result block and gate (gate = 0: the single
+  // pass decides; 1: exact path only), chunk rows no tile writes (~0, filled
+  // by the finish kernel), the single pass's first error, look-back words,
+  // qid shards and unit minima, the exact path's unit minima
+  FillList fl{};
   if (phase != kPhaseFill) {
-    if ((e = hipMemsetAsync(res, 0, 16 * sizeof(uint64_t), s)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(res + 8, 0xFF, sizeof(uint64_t), s)) != hipSuccess) return e;
-    // gate = 0 (fast path decides) or 1 (exact path only)
-    if ((e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(gate), use_fast ? 0 : 1, 1, s)) !=
-        hipSuccess)
-      return e;
+    fill_result(fl, res);
+    fl.gate = gate;
+    fl.gate_v = use_fast ? 0u : 1u;
   }
-  if (phase != kPhaseCount && f.chunk_tab &&
-      (e = hipMemsetAsync(f.chunk_tab, 0xFF, (size_t)f.nchunk * 8 * sizeof(uint64_t), s)) != hipSuccess)
-    return e;  // rows no tile writes are filled by chunk_fixup_kernel
+  if (phase != kPhaseCount) fl.add(f.chunk_tab, (uint64_t)f.nchunk * 8, ~0ull);
+  fl.add(reinterpret_cast<uint64_t *>(f.err), 1, ~0ull);
   if (use_fast) {
-    if ((e = hipMemsetAsync(f.err, 0xFF, sizeof(uint64_t), s)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(f.lb, 0, ((size_t)f.ntiles * fast::kLbWords + 1) * sizeof(uint64_t), s)) != hipSuccess)
-      return e;  // + the ticket word
-    if ((e = hipMemsetAsync(f.qsum, 0, kLabShards * 8 * sizeof(uint64_t), s)) != hipSuccess) return e;
+    fl.add(f.lb, (uint64_t)f.ntiles * fast::kLbWords + 1, 0);  // + the ticket word
+    fl.add(f.qsum, kLabShards * 8, 0);
+    if (phase != kPhaseCount && f.indexing_mode < 0) fl.add(f.umin, (uint64_t)f.nchunk, ~0ull);
+  }
+  if (phase != kPhaseFill && a.indexing_mode < 0) fl.add(a.chunk_min, (uint64_t)a.nchunk, ~0ull);
+  if (!a.ntiles && phase != kPhaseCount) fl.add(a.offset, 1, 0);  // empty input: offset = {0}
+  if ((e = launch_prologue(fl, s)) != hipSuccess) return e;
+  if (use_fast) {
     if (phase == kPhaseCount) {
       prof_mark(0, s, "svm_fast_tile<1>");
       svm_fast_tile<1><<<FSVM_PERSIST ? persistent_grid(svm_fast_tile<1>, f.ntiles) : f.ntiles, fast::kFThreads, 0, s>>>(f);
       prof_mark(1, s, "svm_fast_tile<1>");
     } else {
-      if (f.indexing_mode < 0 &&
-          (e = hipMemsetAsync(f.umin, 0xFF, (size_t)f.nchunk * sizeof(uint64_t), s)) != hipSuccess)
-        return e;
       prof_mark(0, s, "svm_fast_tile<2>");
       svm_fast_tile<2><<<FSVM_PERSIST ? persistent_grid(svm_fast_tile<2>, f.ntiles) : f.ntiles, fast::kFThreads, 0, s>>>(f);
       prof_mark(1, s, "svm_fast_tile<2>");
     }
-    qid_fix_kernel<<<1, 256, 0, s>>>(f.qsum, res, gate, phase != kPhaseCount ? f.chunk_tab : nullptr, f.nchunk);
-  } else if ((e = hipMemsetAsync(f.err, 0xFF, sizeof(uint64_t), s)) != hipSuccess) {
-    return e;
+    // the qid decision (qid_fix_kernel) is folded into the exact count
+    // kernel (a mix hands over) and the finish kernel (every row has a qid);
+    // the fill phase keeps the kernel
+    if (phase == kPhaseFill) qid_fix_kernel<<<1, 256, 0, s>>>(f.qsum, res, gate, f.chunk_tab, f.nchunk);
+  }
+  LibsvmArgs ac = a;  // the exact count pass of a full / count phase: the qid check
+  if (use_fast && phase != kPhaseFill) {
+    ac.qsum = f.qsum;
+    ac.qres = res;
   }
   // ---- exact path, gated on the device flag (early exit when the fast path stood)
-  if (phase != kPhaseFill) {
-    if (a.indexing_mode < 0 &&
-        (e = hipMemsetAsync(a.chunk_min, 0xFF, (size_t)a.nchunk * sizeof(uint64_t), s)) != hipSuccess)
-      return e;
-  } else {
-    reopen_kernel<<<1, 1, 0, s>>>(res, a.offset, a.cap[C_ROWS], gate);
-  }
-  if (!a.ntiles && phase != kPhaseCount && a.offset && (e = hipMemsetAsync(a.offset, 0, 8, s)) != hipSuccess)
-    return e;  // empty input: offset = {0}
+  if (phase == kPhaseFill) reopen_kernel<<<1, 1, 0, s>>>(res, a.offset, a.cap[C_ROWS], gate);
+  // the chunk rows the single pass wrote are reset when it handed over
+  const bool reset_tab = use_fast && phase != kPhaseCount && f.chunk_tab && f.nchunk > 0;
+  uint64_t *rtab = reset_tab ? f.chunk_tab : nullptr;
+  const uint64_t ntab = reset_tab ? (uint64_t)f.nchunk * 8 : 0;
   if (a.ntiles) {
     if (phase != kPhaseFill) {
-      libsvm_tile<1><<<a.ntiles, kThreads, 0, s>>>(a);
+      libsvm_tile<1><<<a.ntiles, kThreads, 0, s>>>(ac);
       tile_scan_kernel<<<1, kThreads, 0, s>>>(a.tile_cnt, const_cast<uint64_t *>(a.tile_base), a.ntiles,
-                                              res, a.offset, a.cap[C_ROWS], gate);
+                                              res, a.offset, a.cap[C_ROWS], gate, rtab, ntab, gate);
       if (phase == kPhaseCount) note_gate_kernel<<<1, 1, 0, s>>>(gate);
     } else {
       // the count phase stood on the single-pass kernel but its write pass
@@ -189,18 +203,16 @@ hipError_t launch_libsvm(const LibsvmArgs &a, const FastSvmArgs &f, bool use_fas
       ra.gate = gate + 2;
       libsvm_tile<1><<<a.ntiles, kThreads, 0, s>>>(ra);
       tile_scan_kernel<<<1, kThreads, 0, s>>>(a.tile_cnt, const_cast<uint64_t *>(a.tile_base), a.ntiles,
-                                              res, a.offset, a.cap[C_ROWS], gate + 2);
+                                              res, a.offset, a.cap[C_ROWS], gate + 2, rtab, ntab, gate);
     }
     if (phase != kPhaseCount) {
-      if (use_fast && f.chunk_tab && f.nchunk > 0)
-        tab_reset_kernel<<<(f.nchunk * 8 + 255) / 256, 256, 0, s>>>(f.chunk_tab, (uint64_t)f.nchunk * 8, gate);
       if (!use_fast) prof_mark(0, s, "libsvm_tile<2>");
       libsvm_tile<2><<<a.ntiles, kThreads, 0, s>>>(a);
       if (!use_fast) prof_mark(1, s, "libsvm_tile<2>");
     }
   }
-  select_kernel<<<1, 1, 0, s>>>(res, gate, f.err);
-  if (phase != kPhaseCount && f.chunk_tab && f.nchunk > 0) chunk_fixup_kernel<<<1, 256, 0, s>>>(f.chunk_tab, f.nchunk, res);
+  finish_kernel<<<1, 256, 0, s>>>(res, gate, f.err, phase != kPhaseCount ? f.chunk_tab : nullptr, f.nchunk,
+                                  use_fast && phase != kPhaseFill ? f.qsum : nullptr);
   if (use_fast && phase != kPhaseCount && f.indexing_mode < 0 &&
       (e = launch_umin_fix(f.index, nullptr, f.wide, f.chunk_tab, f.nchunk, f.umin, res, gate, f.cap[C_INDEX], 0, s)) !=
           hipSuccess)

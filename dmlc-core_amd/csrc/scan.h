@@ -22,7 +22,14 @@ struct Cnt64Add {
 // offset[total_rows] = total index count (the reference's final offset push).
 __global__ void __launch_bounds__(kThreads)
 tile_scan_kernel(const uint64_t *tile_cnt, uint64_t *tile_base, uint32_t ntiles, uint64_t *res,
-                 uint64_t *offset, uint64_t cap_rows, const uint32_t *gate) {
+                 uint64_t *offset, uint64_t cap_rows, const uint32_t *gate, uint64_t *tab = nullptr,
+                 uint64_t ntab = 0, const uint32_t *tab_gate = nullptr) {
+  // before the exact write pass of a call whose single pass handed over:
+  // forget the chunk-table rows it wrote (units the exact kernels never visit
+  // -- no line in them -- then take the next unit's counts in the finish
+  // kernel instead of stale single-pass ones)
+  if (tab && *tab_gate)
+    for (uint64_t i = threadIdx.x; i < ntab; i += blockDim.x) tab[i] = ~0ull;
   if (gate && *gate == 0) return;
   __shared__ uint64_t scratch[kBlockScratchU64];
   DevBlock bk{scratch};
@@ -54,7 +61,7 @@ tile_scan_kernel(const uint64_t *tile_cnt, uint64_t *tile_base, uint32_t ntiles,
 // it -- sources are never copied into, so the two phases do not race.  (A
 // single thread walking the rows backwards took ~160 us on ~500 rows: one
 // dependent global round trip per row.)
-__global__ void __launch_bounds__(256) chunk_fixup_kernel(uint64_t *chunk_tab, int nchunk, const uint64_t *res) {
+__device__ __forceinline__ void chunk_fixup_body(uint64_t *chunk_tab, int nchunk, const uint64_t *res) {
   for (int c = threadIdx.x; c < nchunk; c += blockDim.x) {
     uint64_t *row = chunk_tab + (uint64_t)c * 8;
     if (row[0] != ~0ull) continue;
@@ -74,16 +81,6 @@ __global__ void __launch_bounds__(256) chunk_fixup_kernel(uint64_t *chunk_tab, i
   }
 }
 
-// Before the exact write pass: when the gate handed the input over, forget the
-// chunk-table rows the single-pass kernel wrote (units the exact kernels never
-// visit -- no line in them -- then take the next unit's counts in
-// chunk_fixup_kernel instead of stale single-pass ones).
-__global__ void tab_reset_kernel(uint64_t *tab, uint64_t n, const uint32_t *gate) {
-  if (*gate == 0) return;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
-    tab[i] = ~0ull;
-}
-
 // The fill phase of a COUNT_ONLY -> FILL_ONLY pair reuses the tile bases of
 // the count phase.  When that count ran on the single-pass kernel (gate 0)
 // but the single-pass write kernel then hands over (the kSpinLimit valve sets
@@ -91,6 +88,81 @@ __global__ void tab_reset_kernel(uint64_t *tab, uint64_t n, const uint32_t *gate
 // first.  gate[1] = the gate as the count phase left it; gate[2] = "recount".
 __global__ void note_gate_kernel(uint32_t *gate) { gate[1] = gate[0]; }
 __global__ void recount_flag_kernel(uint32_t *gate) { gate[2] = (gate[0] != 0 && gate[1] == 0) ? 1u : 0u; }
+
+// ---- per-call set-up and finish, one launch each (every kernel boundary on
+// the stream costs a few microseconds: the set-up used to be six memsets and
+// the finish two kernels).  Prologue: fill up to kFillRegions word ranges and
+// set the gate word.
+constexpr int kFillRegions = 10;
+struct FillList {
+  uint64_t *p[kFillRegions];
+  uint64_t n[kFillRegions];
+  uint64_t v[kFillRegions];
+  uint32_t *gate;  // set to gate_v when non-null
+  uint32_t gate_v;
+  int count;
+  DA_HD void add(uint64_t *ptr, uint64_t words, uint64_t value) {
+    if (ptr && words && count < kFillRegions) {
+      p[count] = ptr;
+      n[count] = words;
+      v[count] = value;
+      ++count;
+    }
+  }
+};
+__global__ void __launch_bounds__(256) prologue_kernel(FillList f) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (uint64_t)gridDim.x * blockDim.x;
+  if (t == 0 && f.gate) *f.gate = f.gate_v;
+  for (int r = 0; r < f.count; ++r)
+    for (uint64_t i = t; i < f.n[r]; i += stride) f.p[r][i] = f.v[r];
+}
+inline hipError_t launch_prologue(const FillList &f, hipStream_t s) {
+  uint64_t most = 1;
+  for (int r = 0; r < f.count; ++r) most = f.n[r] > most ? f.n[r] : most;
+  uint64_t blocks = (most + 1023) / 1024;  // four words per thread on the largest range
+  blocks = blocks < 1 ? 1 : (blocks > 1024 ? 1024 : blocks);
+  prologue_kernel<<<(unsigned)blocks, 256, 0, s>>>(f);
+  return hipGetLastError();
+}
+// The result block of a call's first phase: counts 0, first error "none" (~0).
+inline void fill_result(FillList &f, uint64_t *res) {
+  f.add(res, 8, 0);
+  f.add(res + 8, 1, ~0ull);
+  f.add(res + 9, 7, 0);
+}
+
+// Finish: the error of whichever path produced the result (res[8]) and the
+// path (res[9]), then the chunk rows no tile wrote (chunk_fixup_body), one block of 256.
+// With qsum (libsvm after its single pass, full and count phases): first the
+// qid decision when the single pass stood (svm_fast.h qid_decide; a mix was
+// handed over by the exact count kernel): every row has a qid, so the qid
+// count is the row count, in the result and in each written chunk row.
+__global__ void __launch_bounds__(256) finish_kernel(uint64_t *res, const uint32_t *gate,
+                                                     const unsigned long long *ferr, uint64_t *chunk_tab, int nchunk,
+                                                     const uint64_t *qsum = nullptr) {
+  __shared__ int qid_rows;
+  if (threadIdx.x < kWave) {
+    uint64_t t = qsum && *gate == 0 && qsum[1] ? qsum[threadIdx.x * 8] : 0;
+    for (int d = 32; d >= 1; d >>= 1) t += __shfl_xor(t, d, kWave);
+    if (threadIdx.x == 0) {
+      qid_rows = t != 0 && t == res[C_ROWS];
+      if (qid_rows) res[C_QID] = t;
+      if (*gate == 0) res[8] = *ferr;
+      if (res[8] == ~0ull) res[8] = 0;
+      res[9] = *gate;  // dmlc_amd_result.path
+    }
+  }
+  __syncthreads();
+  if (!chunk_tab || nchunk <= 0) return;
+  if (qid_rows) {
+    for (int c = threadIdx.x; c < nchunk; c += blockDim.x) {
+      uint64_t *row = chunk_tab + (uint64_t)c * 8;
+      if (row[C_ROWS] != ~0ull) row[C_QID] = row[C_ROWS];
+    }
+    __syncthreads();
+  }
+  chunk_fixup_body(chunk_tab, nchunk, res);
+}
 
 }  // namespace
 }  // namespace dmlc_amd

@@ -51,7 +51,7 @@ DA_HD bool qid_decide(uint64_t total, uint64_t *res, uint32_t *gate) {
 // each ParseBlock unit holding a 0 id (umin[u] = 0, libfm: among fields and
 // indices; ~0 otherwise); afterwards every id of a unit without a 0 id (its
 // minimum is > 0) drops by one.  The units' index ranges are the chunk table's index column (tab,
-// nunit rows of 8, complete after chunk_fixup_kernel).  Entries [lo, hi) of
+// nunit rows of 8, complete after finish_kernel).  Entries [lo, hi) of
 // the index array (and the field array, when set), stride `step` from lo.
 DA_HD int unit_of_entry(const uint64_t *tab, int nunit, uint64_t i) {  // last unit whose range starts <= i
   int lo = 0, hi = nunit;
@@ -1073,7 +1073,10 @@ DA_HDF uint32_t tile_p(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k, Sta
   if (tid == 0) {
     publish_aggregate(a.lb, a.ntiles, k, cnt4);
     if (sh.c.bad) atomic_or_u32(a.gate, 1u);
-    if (!FM && sh.nq) atomic_add_u64(a.qsum + (k % kLabShards) * 8, sh.nq);  // qid_fix_kernel's sum
+    if (!FM && sh.nq) {  // the qid decision's sum (libsvm.hip), and the "some qid" word
+      atomic_add_u64(a.qsum + (k % kLabShards) * 8, sh.nq);
+      if (load_agent_u64(a.qsum + 1) == 0) store_agent_u64(a.qsum + 1, 1);
+    }
   }
   const uint64_t P = t.tlo + (uint64_t)tid * kSegB;
   const bool one_chunk = sh.c.ncs == 0;  // no chunk boundary before cnext

@@ -152,7 +152,7 @@ void tile_scan(const std::vector<uint64_t> &cnt, std::vector<uint64_t> &base, ui
   for (int i = 0; i < C_N; ++i) res[i] = run[i];
 }
 
-// mirrors the launchers' chunk-table pre-fill and chunk_fixup_kernel (scan.h)
+// mirrors the launchers' chunk-table pre-fill and finish_kernel (scan.h chunk_fixup_body)
 void chunk_prefill(uint64_t *tab, int nchunk) {
   if (tab) std::memset(tab, 0xFF, (size_t)(nchunk > 0 ? nchunk : 0) * 8 * sizeof(uint64_t));
 }
@@ -317,7 +317,7 @@ extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *c
       }
       tile_scan(tile_cnt, tile_base, ntiles, res);
       if (!count_only && out->offset && res[C_ROWS] < out->cap[C_ROWS] + 1) out->offset[res[C_ROWS]] = res[C_INDEX];
-      if (!count_only) chunk_prefill(chunk_table, nchunks);  // tab_reset_kernel (scan.h)
+      if (!count_only) chunk_prefill(chunk_table, nchunks);  // the chunk-table reset in tile_scan_kernel (scan.h)
       if (!count_only)
         for (uint64_t k = 0; k < ntiles; ++k) {
           svm::Shared *sh = new svm::Shared;
@@ -330,7 +330,7 @@ extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *c
         }
     } else {
       res[8] = ferr;
-      if (imin && !count_only && ftab) {  // chunk_fixup_kernel, then umin_fix_kernel (svm_fast.h)
+      if (imin && !count_only && ftab) {  // finish_kernel, then umin_fix_kernel (svm_fast.h)
         chunk_fixup(ftab, nchunks, res);
         uint64_t tot = res[C_INDEX] < out->cap[C_INDEX] ? res[C_INDEX] : out->cap[C_INDEX];  // umin_fix_kernel's clamp
         if (fm && tot > out->cap[C_FIELD]) tot = out->cap[C_FIELD];
@@ -451,7 +451,7 @@ extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *c
     }
     tile_scan(tile_cnt, tile_base, ntiles, res);
     if (!count_only && out->offset && res[C_ROWS] < out->cap[C_ROWS] + 1) out->offset[res[C_ROWS]] = res[C_INDEX];
-    if (!count_only) chunk_prefill(chunk_table, nchunks);  // tab_reset_kernel (scan.h)
+    if (!count_only) chunk_prefill(chunk_table, nchunks);  // the chunk-table reset in tile_scan_kernel (scan.h)
     if (!count_only)
       for (uint64_t k = 0; k < ntiles; ++k) {
         csv::Shared *sh = new csv::Shared;
