@@ -138,6 +138,15 @@ constexpr int kListCap = (int)(sizeof(Planes) / sizeof(uint16_t));
 // before its last segment starts (a segment holds <= 64 run starts)
 constexpr uint32_t kPassRuns = (uint32_t)kListCap - kSegB;
 
+// Per-line fallback (dirty_lines): a tile takes the lines holding bytes
+// outside the grammar -- after its comments are blanked -- from a byte walk of
+// the reference's line parse, at most kDirtyLines lines of at most
+// kDirtyMaxLine bytes and kDirtyEntries runs in the tile.
+constexpr int kDirtyLines = 4;
+constexpr int kDirtyEntries = 40;
+constexpr uint64_t kDirtyMaxLine = 256;
+constexpr int kPendWords = (kTile / kPassRuns + 2) > kFWaves ? (kTile / kPassRuns + 2) : kFWaves;
+
 struct Shared {  // LDS of one workgroup
   TileCommon c;
   uint32_t cls[kClsEntries];  // byte class table (fast_common.h class_of)
@@ -147,11 +156,15 @@ struct Shared {  // LDS of one workgroup
     uint16_t lst[kListCap];
   } u;
   uint32_t gw[2 * kFThreads + 2];  // digit plane as words: 2t, 2t+1 segment t; 2 kFThreads: the post-halo
-  uint64_t pend[kTile / kPassRuns + 2];  // packed inclusive counts at the end of each pass
+  uint64_t pend[kPendWords];  // packed inclusive counts at the end of each pass (dirty_lines: wave masks)
+  uint64_t prebad;            // pre-halo bytes outside the grammar (dirty_lines)
   uint32_t npass;
   uint32_t next;   // persistent form: the next tile id
   uint32_t nq;     // qid runs of the tile
   uint32_t hashy;  // a byte outside the grammar: comments to blank (pass 1)
+  uint32_t ndl, ndr, dgate, nseg;
+  uint32_t dl[kDirtyEntries];      // dirty lines' runs in the tile: tile offset | kind << 16
+  int32_t dr[2 * kDirtyLines];     // dirty lines [lbegin, lend], tile-relative
 };
 
 struct Tile {
@@ -890,6 +903,7 @@ DA_HDF uint32_t classify_tile(const Tile &t, Shared &sh, int tid, At at, bool fi
     memcpy(&x, sh.c.text + (kPre - kSegB) + 4 * tid, 4);
     const Nib b = classify_dword_lut(x, sh.cls);
     if (!FM && first && b.bad) sh.hashy = 1;
+    if (!FM && b.bad) atomic_or_u64(&sh.prebad, (uint64_t)((b.g & ~b.d) | b.hi) << (4 * tid));  // (dirty_lines)
     uint64_t bn = b.n, bc = b.c;
     const uint64_t P0 = t.tlo - kSegB + 4 * tid;
     if (!FM && ((bn & bc) || (bc & 1))) {  // the bytes' owner tile checks them; here only their planes
@@ -904,27 +918,110 @@ DA_HDF uint32_t classify_tile(const Tile &t, Shared &sh, int tid, At at, bool fi
   return bad;
 }
 
-// Pass 1 (libsvm): blank the comments and classify again what changed; all
-// threads, after the chunk list is known.  bad0: the segment's pass-0 flag.
-// (inline: out of line, the call frame's spills cost the kernel 2.2x, 3.97 ms
-// on config 2)
-template <class BK>
-DA_HDF uint32_t comments_reclassify(const Tile t, Shared &sh, uint32_t bad0, BK &bk) {
+// ---- per-line fallback.  A line holding bytes outside the grammar (after
+// the tile's comments are blanked) -- a "# header" line of the next file that
+// InputSplit put mid-chunk (input_split_base.cc:204-210), which the reference
+// reads as a row (libsvm_parser.h:91-104), a word in a value -- takes its run
+// positions from walk_line, the reference's line parse; the tile blanks the
+// line in its staged text (classification and roles see an empty line), ORs
+// the walked runs into its role masks and decodes them with the byte decoders.
+// Everything else about the tile is unchanged.  A line the tile cannot walk
+// cheaply or fully gates the call over to the exact kernels as before.
+enum : uint32_t { DK_L = 1, DK_W = 2, DK_I = 3, DK_V = 4, DK_Q = 5 };
+// ParseBlock's line from lb (libsvm_parser.h:85-160) as one byte loop over
+// the staged text (offsets into txt): IgnoreCommentAndBlank (:67-83) at its
+// start and at every pair end, ParsePair (strtonum.h:667-703) for
+// label[:weight] and each index[:value] -- non-digitchars skipped to a run,
+// blanks to a ':' -- and "qid:" after the label pair's spaces (:119-132).
+// emit(kind, offset) in line order at the run each value is decoded from (a
+// ':' at the line end: the line end itself).  The line ends at the first
+// '\n' / '\r' after lb or at ue; returns that end, or -1 past lim.
+// The staged bytes read a 4-byte word at a time (one LDS round trip per four
+// bytes of a serial walk instead of one per byte).
+struct WordCache {
+  const uint8_t *txt;
+  int32_t at = -4;
+  uint32_t w = 0;
+  DA_HD uint32_t operator()(int32_t p) {
+    if ((p & ~3) != at) {
+      at = p & ~3;
+      w = *reinterpret_cast<const uint32_t *>(txt + at);
+    }
+    return (w >> (8 * (p & 3))) & 0xFFu;
+  }
+};
+template <class Emit>
+DA_HD int32_t walk_line(const uint8_t *txt, int32_t lb, int32_t ue, int32_t lim, Emit emit) {
+  int32_t le = lb + 1;
+  {  // the line end: a word at a time
+    WordCache wc{txt};
+    while (le < ue && !is_nl(wc(le))) {
+      if (++le > lim) return -1;
+    }
+  }
+  if (le > ue) le = ue;
+  WordCache byte{txt};
+  enum : uint32_t { ICB, SEEK, RUN, BL, SEEK2, RUN2, QSP };
+  uint32_t st = ICB;
+  bool head = true;  // the label pair; then the features
+  for (int32_t p = lb; p < le;) {
+    const uint32_t b = byte(p);
+    if (st == ICB) {  // IgnoreCommentAndBlank
+      if (b == '#') return le;
+      if (is_blank(b)) ++p;
+      else st = SEEK;
+    } else if (st == SEEK || st == SEEK2) {  // ParsePair: to the next run
+      if (is_digitchar(b)) {
+        emit(st == SEEK ? (head ? DK_L : DK_I) : (head ? DK_W : DK_V), p);
+        st = st == SEEK ? RUN : RUN2;
+      } else {
+        ++p;
+      }
+    } else if (st == RUN || st == RUN2) {  // the run (decoded by the caller)
+      if (is_digitchar(b)) {
+        ++p;
+      } else if (st == RUN) {
+        st = BL;
+      } else {  // the pair's end (after a label pair: its qid)
+        st = head ? QSP : ICB;
+        head = false;
+      }
+    } else if (st == BL) {  // blanks, then a ':' or the pair's end
+      if (is_blank(b)) {
+        ++p;
+      } else if (b == ':') {
+        ++p;
+        st = SEEK2;
+      } else {
+        st = head ? QSP : ICB;
+        head = false;
+      }
+    } else {  // QSP: spaces, then "qid:<digits>"
+      if (b == ' ') {
+        ++p;
+      } else {
+        if (p + 3 < le && b == 'q' && byte(p + 1) == 'i' && byte(p + 2) == 'd' && byte(p + 3) == ':') {
+          p += 4;
+          emit(DK_Q, p);
+          while (p < le && is_digitchar(byte(p))) ++p;
+        }
+        st = ICB;
+      }
+    }
+  }
+  if (st == SEEK2) emit(head ? DK_W : DK_V, le);  // "x:" at the line end: the value after it
+  return le;
+}
+
+// The tile's segments (and halos) whose flag is set, classified again from
+// the staged text (after blanking), each by its wave: lane = byte, one ballot
+// per plane; parts: classify_tile's halo bits.  Returns the segment's flag.
+template <class BK, class At>
+DA_HDF uint32_t reclassify_blanked(const Tile &t, Shared &sh, uint32_t bad, bool changed, uint32_t parts, BK &bk,
+                                   At at) {
   const int tid = bk.tid();
   const uint32_t lane = (uint32_t)tid & (kWave - 1), wbase = (uint32_t)tid - lane;
-  const FastSvmArgs &a = *t.a;
-  const uint32_t e = comment_erase(t.tlo, t.thi, a.n, sh.c, &sh.hashy, bk, sh.u.m.d[tid + 1], sh.u.m.n[tid + 1],
-                                   sh.u.m.c[tid + 1], bad0 != 0);
-  if (e & 12u) atomic_or_u32(&sh.hashy, (e & 12u) << 1);  // pre-halo / post-halo blanked: note bits 3 / 4
-  if (tid == 0 && (e & 4u)) sh.u.m.d[0] = sh.u.m.n[0] = sh.u.m.c[0] = 0;
-  bk.sync();
-  auto at = [&](uint64_t p) -> uint32_t {
-    if (p >= a.n) return 0u;
-    return p + kPre >= t.tlo ? (uint32_t)sh.c.text[p - t.tlo + kPre] : gbyte(a.text, p);
-  };
-  // the blanked segments classified again, each by its wave (lane = byte)
-  uint32_t bad = bad0;
-  for (uint64_t m = bk.ballot((e >> 1) & 1u); m; m &= m - 1) {  // wave-uniform
+  for (uint64_t m = bk.ballot(changed); m; m &= m - 1) {  // wave-uniform
     const uint32_t sg = wbase + (uint32_t)ctz64(m);
     const uint32_t b = sh.c.text[kPre + sg * kSegB + lane];
     const uint32_t x = b >= 0x80u ? 0x00000100u : sh.cls[b];  // (>= 0x80: outside the grammar)
@@ -936,10 +1033,276 @@ DA_HDF uint32_t comments_reclassify(const Tile t, Shared &sh, uint32_t bad0, BK 
     mm.bad = (mm.g & ~mm.d) != 0;
     if (sg == (uint32_t)tid) bad = commit_seg<false>(t, sh, tid, at, false, mm);
   }
-  const uint32_t note = sh.hashy;
-  const uint32_t parts = (note >> 2) & 6u;  // the halos (rare): classify_tile's lanes
   if (parts) (void)classify_tile<false>(t, sh, tid, at, false, parts);
   bk.sync();
+  return bad;
+}
+
+// Bytes outside the grammar in segment s (G without D; the qid letters are N
+// and C) and in the pre-halo.
+DA_HD uint64_t outside_mask(const Tile &t, const Shared &sh, int s) {
+  const uint64_t P = t.tlo + (uint64_t)s * kSegB;
+  if (P >= t.a->n) return 0;
+  const uint64_t g = sh.gw[2 * s] | ((uint64_t)sh.gw[2 * s + 1] << 32);
+  return g & ~sh.u.m.d[s + 1];
+}
+
+// After the comment pass of a tile holding bytes outside the grammar: find
+// their lines, walk them (thread 0, in text order), blank them and classify
+// the blanked segments again.  Returns the segment's flag, with bit 0 set
+// when the call must go to the exact kernels.
+template <class BK, class At>
+DA_HDF uint32_t dirty_lines(const Tile &t, Shared &sh, uint32_t bad, BK &bk, At at, uint32_t k) {
+  (void)k;  // (phase stamps of the diagnostic build)
+  const int tid = bk.tid();
+  const uint32_t lane = (uint32_t)tid & (kWave - 1);
+  const uint64_t wm = bk.ballot(outside_mask(t, sh, tid) != 0);
+  if (lane == 0) sh.pend[tid / kWave] = wm;
+  bk.sync();
+  uint64_t any = sh.prebad;
+  for (int w = 0; w < kFWaves; ++w) any |= sh.pend[w];
+  if (!any) return bad;  // block-uniform
+  const uint64_t n = t.a->n;
+  const uint64_t slo = t.tlo >= (uint64_t)kPre ? t.tlo - kPre : 0;  // staged range
+  const uint64_t shi = mn<uint64_t>(t.tlo + kTile + kPost, n);
+  if (tid == 0) {
+    uint32_t gate = 0, nl = 0, ne = 0;
+    uint64_t cover = 0;
+    const uint8_t *txt = sh.c.text;  // staged offset i <-> position tlo - kPre + i
+    const int64_t base = (int64_t)t.tlo - kPre;
+    const int32_t s_lo = (int32_t)((int64_t)slo - base), s_hi = (int32_t)((int64_t)shi - base);
+    auto visit = [&](uint64_t x) {
+      if (gate || x < cover) return;
+      const uint64_t F = t.floor_of(x);
+      if (F > x) {  // a pre-halo byte whose line ends at a unit start <= tlo
+        cover = F;
+        return;
+      }
+      const int32_t xs = (int32_t)((int64_t)x - base);
+      if (x < t.tlo) {  // a pre-halo byte: only a line reaching into the tile is this tile's
+        for (int32_t i = xs + 1; i <= kPre; ++i)
+          if (is_nl(txt[i])) {
+            cover = (uint64_t)(base + i);
+            return;
+          }
+      }
+      const int64_t fs = (int64_t)F - base;  // the unit start (may lie before the staged bytes)
+      const int32_t stop = fs > (int64_t)s_lo ? (int32_t)fs : s_lo;
+      int32_t lb = xs;  // the newline opening x's line, or its unit start
+      WordCache wc{txt};
+      while (lb > stop && !is_nl(wc(lb))) --lb;
+      // no newline down to the staged start: the line starts before the staged bytes
+      if ((!is_nl(wc(lb)) && (int64_t)lb != fs) || xs - lb > (int32_t)kDirtyMaxLine) {
+        gate = 1;
+        return;
+      }
+      const uint64_t ue = mn<uint64_t>(t.next_cs(x), n);
+      const int32_t ues = (int32_t)mn<int64_t>((int64_t)ue - base, s_hi);
+      const int32_t le = walk_line(txt, lb, ues, mn<int32_t>(lb + (int32_t)kDirtyMaxLine, s_hi),
+                                   [&](uint32_t k, int32_t o) {
+                                     if (k == DK_Q || ne >= (uint32_t)kDirtyEntries || o >= ues || is_nl(txt[o])) {
+                                       gate = 1;  // a qid, too many runs, or a value read past the line end
+                                       return;
+                                     }
+                                     sh.dl[ne++] = (uint32_t)o | (k << 16);  // staged offset
+                                   });
+      // unwalkable here: too long, ending past the staged bytes, or at a unit
+      // end inside a line (the decoders would read on into the next unit)
+      if (le < 0 || (le == ues && (uint64_t)(base + le) < n && !is_nl(txt[le]))) {
+        gate = 1;
+        return;
+      }
+      const uint64_t lend = (uint64_t)(base + le), lbg = (uint64_t)(base + lb);
+      cover = lend;
+      if (lend <= t.tlo) return;  // the previous tile's line
+      // a line running on into the next tile must show it one of its bytes
+      // outside the grammar in its pre-halo (the last 64 bytes of this tile)
+      if (lend > t.thi && t.thi < n) {
+        const uint64_t last = outside_mask(t, sh, kFThreads - 1);
+        const uint64_t P = t.tlo + (uint64_t)(kFThreads - 1) * kSegB;
+        const uint64_t from = lbg > P ? lbg - P : 0;
+        if (!(last & (~0ull << from))) {
+          gate = 1;
+          return;
+        }
+      }
+      if (nl >= (uint32_t)kDirtyLines) {
+        gate = 1;
+        return;
+      }
+      sh.dr[2 * nl] = (int32_t)((int64_t)lbg - (int64_t)t.tlo);
+      sh.dr[2 * nl + 1] = (int32_t)(lend - t.tlo);
+      ++nl;
+    };
+    for (uint64_t m = sh.prebad; m && t.tlo >= (uint64_t)kPre; m &= m - 1) visit(t.tlo - kPre + ctz64(m));
+    for (int w = 0; w < kFWaves; ++w)
+      for (uint64_t m = sh.pend[w]; m; m &= m - 1) {
+        const int s = w * kWave + (int)ctz64(m);
+        const uint64_t P = t.tlo + (uint64_t)s * kSegB;
+        for (uint64_t b = outside_mask(t, sh, s); b; b &= b - 1) visit(P + ctz64(b));
+      }
+    sh.ndl = gate ? 0u : ne;
+    sh.ndr = gate ? 0u : nl;
+    sh.dgate = gate;
+  }
+  bk.sync();
+  FAST_STAMP(k, 13);
+  if (sh.dgate) return bad | 1u;
+  const uint32_t nr = sh.ndr;
+  if (nr == 0) return bad;
+  // blank the lines (from the byte after the opening newline, or from the
+  // unit start) in the staged text: my segment; wave 0 the pre-halo, the
+  // last wave the post-halo
+  auto blank_in = [&](uint64_t lo, uint64_t hi) -> bool {  // my staged bytes [lo, hi) of the lines
+    bool ch = false;
+    for (uint32_t r = 0; r < nr; ++r) {
+      const uint64_t lb = (uint64_t)((int64_t)t.tlo + sh.dr[2 * r]), le = t.tlo + (uint64_t)sh.dr[2 * r + 1];
+      const uint64_t b0 = is_nl(at(lb)) && t.floor_of(lb) != lb ? lb + 1 : lb;
+      const uint64_t a0 = b0 > lo ? b0 : lo, a1 = le < hi ? le : hi;
+      for (uint64_t p = a0; p < a1; ++p) {
+        sh.c.text[p - t.tlo + kPre] = ' ';
+        ch = true;
+      }
+    }
+    return ch;
+  };
+  const uint64_t P = t.tlo + (uint64_t)tid * kSegB;
+  const bool changed = P < n && blank_in(P, mn<uint64_t>(P + kSegB, n));
+  uint32_t parts = 0;
+  if (tid < kWave && t.tlo > 0) {
+    const uint64_t x = t.tlo - kPre + lane;
+    if (x >= slo && blank_in(x, x + 1)) parts |= 2u;
+  }
+  if (tid >= kFThreads - kWave) {
+    for (uint64_t x = t.thi + lane; x < shi; x += kWave)
+      if (blank_in(x, x + 1)) parts |= 4u;
+  }
+  const uint64_t pm = bk.ballot((parts & 2u) != 0), qm = bk.ballot((parts & 4u) != 0);
+  parts = (pm ? 2u : 0u) | (qm ? 4u : 0u);  // wave-level; made block-level below
+  if (parts) atomic_or_u32(&sh.hashy, parts << 8);
+  bk.sync();
+  parts = (sh.hashy >> 8) & 6u;
+  if (tid == 0 && (parts & 2u)) {
+    sh.u.m.d[0] = sh.u.m.n[0] = sh.u.m.c[0] = 0;
+    sh.prebad = 0;
+  }
+  bk.sync();
+  bad = reclassify_blanked(t, sh, bad, changed, parts, bk, at);
+  // the lines' bytes back for the decoders (index windows: exact on any run
+  // of digitchars; floats are decoded again at the end), digit-plane bits
+  // from the bytes themselves (the table's G also marks bytes outside the
+  // grammar)
+  // (the bytes come back from global memory in 16-byte loads, all in flight
+  // at once: a byte loop waited for one round trip per byte)
+  auto restore = [&](uint64_t lo, uint64_t hi, uint64_t *dig) -> uint64_t {  // [lo, hi): 64 bytes from lo (16-aligned)
+    uint64_t rm = 0;
+    for (uint32_t r = 0; r < nr; ++r) {
+      const uint64_t lb = (uint64_t)((int64_t)t.tlo + sh.dr[2 * r]), le = t.tlo + (uint64_t)sh.dr[2 * r + 1];
+      const uint64_t b0 = is_nl(at(lb)) && t.floor_of(lb) != lb ? lb + 1 : lb;
+      const uint64_t a0 = b0 > lo ? b0 : lo, a1 = le < hi ? le : hi;
+      if (a0 < a1) rm |= (a1 - lo >= 64 ? ~0ull : (1ull << (a1 - lo)) - 1) & ~((1ull << (a0 - lo)) - 1);
+    }
+    if (!rm) return 0;
+    uint32_t w[16];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint64_t g = lo + 16 * (uint64_t)q;
+      if (g + 16 <= n) {
+        load16(t.a->text + g, w + 4 * q);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          uint32_t x = 0;
+          for (int b = 0; b < 4; ++b) {
+            const uint64_t pp = g + 4 * j + b;
+            x |= (pp < n ? (uint32_t)gbyte(t.a->text, pp) : 0u) << (8 * b);
+          }
+          w[4 * q + j] = x;
+        }
+      }
+    }
+    uint32_t *lw = reinterpret_cast<uint32_t *>(sh.c.text + (lo - t.tlo + kPre));
+    uint64_t dg = 0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const uint32_t nib = (uint32_t)(rm >> (4 * q)) & 0xFu;
+      if (!nib) continue;
+      const uint32_t bm = ((nib * 0x00204081u) & 0x01010101u) * 0xFFu, x = w[q];
+      lw[q] = (lw[q] & ~bm) | (x & bm);
+      const uint32_t d = ((x | 0x80808080u) - 0x30303030u) & ~((x | 0x80808080u) - 0x3A3A3A3Au) & ~x & 0x80808080u;
+      dg |= (uint64_t)(hi_nib(d) & nib) << (4 * q);
+    }
+    *dig = dg;
+    return rm;
+  };
+  if (changed) {
+    uint64_t dig = 0;
+    const uint64_t rm = restore(P, mn<uint64_t>(P + kSegB, n), &dig);
+    const uint64_t g = ((sh.gw[2 * tid] | ((uint64_t)sh.gw[2 * tid + 1] << 32)) & ~rm) | dig;
+    sh.gw[2 * tid] = (uint32_t)g;
+    sh.gw[2 * tid + 1] = (uint32_t)(g >> 32);
+  }
+  if (parts & 4u) {  // the post-halo (kPost = 128 bytes): two lanes of the last wave, 64 bytes each
+    if (tid >= kFThreads - 2) {
+      const uint64_t lo = t.thi + (uint64_t)(tid - (kFThreads - 2)) * kSegB;
+      uint64_t dig = 0;
+      const uint64_t rm = lo < shi ? restore(lo, mn<uint64_t>(lo + kSegB, shi), &dig) : 0;
+      if (tid == kFThreads - 2) sh.gw[2 * kFThreads] = (uint32_t)((sh.gw[2 * kFThreads] & ~rm) | dig);
+    }
+  }
+  // the walked runs into the (blanked) planes as one-byte runs whose gaps make
+  // the role arithmetic read them as walked: a ':' before a weight or value;
+  // a label follows its line's newline or unit start (not blanked)
+  {
+    const uint32_t ne = sh.ndl;
+    const int32_t s0 = kPre + tid * kSegB;  // my segment's staged offsets; the pre-halo: thread 0's slot 0
+    uint64_t dd = 0, cc = 0, hd = 0, hc = 0;
+    for (uint32_t i = 0; i < ne; ++i) {
+      const uint32_t e = sh.dl[i];
+      const int32_t o = (int32_t)(e & 0xFFFFu);
+      const uint32_t kd = e >> 16;
+      const bool kv = kd == DK_W || kd == DK_V;
+      if (o >= s0 && o < s0 + kSegB) dd |= 1ull << (o - s0);
+      if (kv && o - 1 >= s0 && o - 1 < s0 + kSegB) cc |= 1ull << (o - 1 - s0);
+      if (tid == 0 && o < kPre) hd |= 1ull << o;
+      if (tid == 0 && kv && o - 1 >= 0 && o - 1 < kPre) hc |= 1ull << (o - 1);
+    }
+    if (dd | cc) {
+      sh.u.m.d[tid + 1] |= dd;
+      sh.u.m.c[tid + 1] |= cc;
+    }
+    if (hd | hc) {
+      sh.u.m.d[0] |= hd;
+      sh.u.m.c[0] |= hc;
+    }
+  }
+  bk.sync();
+  return bad;
+}
+
+// Pass 1 (libsvm): blank the comments and classify again what changed; all
+// threads, after the chunk list is known.  bad0: the segment's pass-0 flag.
+// (inline: out of line, the call frame's spills cost the kernel 2.2x, 3.97 ms
+// on config 2)
+template <class BK>
+DA_HDF uint32_t comments_reclassify(const Tile t, Shared &sh, uint32_t bad0, BK &bk) {
+  const int tid = bk.tid();
+  const FastSvmArgs &a = *t.a;
+  const uint32_t e = comment_erase(t.tlo, t.thi, a.n, sh.c, &sh.hashy, bk, sh.u.m.d[tid + 1], sh.u.m.n[tid + 1],
+                                   sh.u.m.c[tid + 1], bad0 != 0);
+  if (e & 12u) atomic_or_u32(&sh.hashy, (e & 12u) << 1);  // pre-halo / post-halo blanked: note bits 3 / 4
+  if (tid == 0 && (e & 4u)) {
+    sh.u.m.d[0] = sh.u.m.n[0] = sh.u.m.c[0] = 0;
+    sh.prebad = 0;
+  }
+  bk.sync();
+  auto at = [&](uint64_t p) -> uint32_t {
+    if (p >= a.n) return 0u;
+    return p + kPre >= t.tlo ? (uint32_t)sh.c.text[p - t.tlo + kPre] : gbyte(a.text, p);
+  };
+  // the blanked segments classified again, each by its wave (lane = byte)
+  const uint32_t parts = (sh.hashy >> 2) & 6u;  // the halos (rare): classify_tile's lanes
+  const uint32_t bad = reclassify_blanked(t, sh, bad0, (e >> 1) & 1u, parts, bk, at);
   return bad | (e & 1u);
 }
 
@@ -1000,6 +1363,8 @@ DA_HDF uint32_t tile_p(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k, Sta
     sh.u.m.d[0] = sh.u.m.n[0] = sh.u.m.c[0] = 0;
     sh.nq = 0;
     sh.hashy = 0;
+    sh.prebad = 0;
+    sh.ndl = sh.ndr = sh.nseg = sh.dgate = 0;
   }
   if (!PERSIST) init_tables(sh, bk);
   stage_commit(a.text, a.n, t.tlo, sr, sh.c, bk);
@@ -1024,7 +1389,47 @@ DA_HDF uint32_t tile_p(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k, Sta
   bk.sync();
   // a byte outside the grammar ('#' among them) in the tile or in the pre-halo:
   // blank the comments and classify again (block-uniform, libsvm only)
-  if (!FM && __builtin_expect(sh.hashy != 0, 0)) bad = comments_reclassify(t, sh, bad, bk);
+  if (!FM && __builtin_expect(sh.hashy != 0, 0)) {
+    // The comment pass first, unless at most two segments (the pre-halo
+    // counting as one) hold bytes outside the grammar and every '#' among
+    // them opens a line (only blanks back to a newline: no comment to the
+    // reference, libsvm_parser.h:91-96) -- a file header, one odd line:
+    // then the walk takes their lines alone.
+    const uint64_t om = outside_mask(t, sh, tid);
+    const uint64_t wm = bk.ballot(om != 0);
+    if ((tid & (kWave - 1)) == 0 && wm) atomic_add_u32(&sh.nseg, (uint32_t)popc64(wm));
+    if (tid == 0 && sh.prebad) atomic_add_u32(&sh.nseg, 1u);
+    bk.sync();
+    if (sh.nseg <= 2u) {  // block-uniform: does every '#' of those segments open a line?
+      // (thread 0 also takes the pre-halo's bytes, first)
+      const bool pre = tid == 0 && sh.prebad && t.tlo >= (uint64_t)kPre;
+      if (om || pre) {
+        const uint64_t slo = t.tlo >= (uint64_t)kPre ? t.tlo - kPre : 0;
+        uint64_t P = pre ? slo : t.tlo + (uint64_t)tid * kSegB, m = pre ? sh.prebad : om, rest = pre ? om : 0;
+        for (;; m &= m - 1) {
+          if (!m) {
+            if (!rest) break;
+            m = rest;
+            rest = 0;
+            P = t.tlo;
+          }
+          const uint64_t x = P + ctz64(m);
+          if (at(x) != '#') continue;
+          uint64_t y = x;
+          while (y > slo && is_blank(at(y - 1))) --y;
+          if (y == 0 || !is_nl(at(y - 1)) || t.is_cs(y)) {  // a comment, or not a line-start '#'
+            atomic_or_u32(&sh.dgate, 1u);  // (dirty_lines sets it again later)
+            break;
+          }
+        }
+      }
+      bk.sync();
+    }
+    if (sh.nseg > 2u || sh.dgate) bad = comments_reclassify(t, sh, bad, bk);
+    FAST_STAMP(k, 12);
+    bad = dirty_lines(t, sh, bad, bk, at, k);  // lines still holding bytes outside the grammar
+    FAST_STAMP(k, 14);
+  }
   if (tid == 0) bad |= sh.c.toomany;
   FAST_STAMP(k, 3);
 #if defined(FSVM_ABL_STOP) && FSVM_ABL_STOP == 1  // timing ablation only: stage + classify
@@ -1100,6 +1505,15 @@ DA_HDF uint32_t tile_p(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k, Sta
   // The decoders take the run's tile offset o (the run starts at tlo + o).
   // win_*: the branch-free window form; *ok = false sends the run to the
   // byte decoders (slow_*), which also raise the sign error.
+  // a float of a walked line (dirty_lines) takes the byte decoder: its window
+  // need not look like the grammar's numbers (indices do not: any digitchar
+  // run reads as ParseUnsignedInt reads it)
+  const uint32_t ndr = FM ? 0u : sh.ndr;
+  auto in_dirty = [&](uint32_t o) -> bool {
+    for (uint32_t r = 0; r < ndr; ++r)
+      if ((int32_t)o >= sh.dr[2 * r] && (int32_t)o < sh.dr[2 * r + 1]) return true;
+    return false;
+  };
   auto win_float = [&](uint32_t o, bool *ok) -> float {
 #ifdef FSVM_ABL_NODEC  // timing ablation only (tools/build_variants.sh), never shipped
     *ok = true;
@@ -1109,7 +1523,7 @@ DA_HDF uint32_t tile_p(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k, Sta
     const uint32_t w4[4] = {(uint32_t)wq.lo, (uint32_t)(wq.lo >> 32), (uint32_t)wq.hi, (uint32_t)(wq.hi >> 32)};
     bool k1;
     const float v = wfloat32m(w4, ndig_at(o), sh.dt, &k1);
-    *ok = k1 && o + 16u <= limr_of(o);
+    *ok = k1 && o + 16u <= limr_of(o) && (ndr == 0 || !in_dirty(o));
     return v;
   };
   // the id as read (<= 8 digits: 32 bits); ids_of applies indexing_mode > 0

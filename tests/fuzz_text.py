@@ -425,3 +425,39 @@ def blank_csv(rng, nlines, maxcols=30, delim=",", ints=False, violate=False):
         out.append(line)
     seps = ["\n"] * 10 + ["\r\n", "\n\n"]
     return "".join(line + seps[int(rng.integers(0, len(seps)))] for line in out).encode("latin-1")
+
+
+DIRTY_LINES = ["# synth libsvm shard", "# hdr", "#!", "junk", "@@@", "7 abc 3:4", "x 1:2 3:4", "5 1:0.5 zz 2:7",
+               "1 2:3 # a comment x", "   hdr  ", "8 qid-less 4:1", "3 1:2 ~ 5:6", "0 1:0.25 2:", "2 !1:3",
+               "9 3:nan 4:1", "4 1:inf", "6 NaN(1):2", "1 2:0.5 3:-inf"]
+
+
+def dirty_libsvm(rng, nbytes, rate=0.002, long_frac=0.0, near_tile_end=False):
+    """Uniform-grammar libsvm rows (about nbytes) with lines holding bytes
+    outside the grammar -- "# header" lines of the next file after InputSplit's
+    '\\n' between files (input_split_base.cc:204-210), words, stray symbols,
+    inf / nan values -- at a share `rate` of the lines; long_frac: share of
+    them longer than 256 bytes.  near_tile_end: put dirty lines across and
+    near the 16 KiB single-pass tile ends."""
+    body = uniform_libsvm(rng, max(1, nbytes // 60), 12).replace(b"\r", b"\n")
+    lines = body.split(b"\n")
+    out = []
+    pos = 0
+    for ln in lines:
+        if rng.random() < rate:
+            d = DIRTY_LINES[int(rng.integers(0, len(DIRTY_LINES)))].encode()
+            if rng.random() < long_frac:
+                d = d + b" " + b"1:2 " * int(rng.integers(70, 120))
+            if rng.random() < 0.5:
+                d = b"\n" + d  # the empty line InputSplit leaves between files
+            if near_tile_end:
+                t_end = (pos // 16384 + 1) * 16384
+                gap = t_end - pos - int(rng.integers(-40, 100))
+                if 0 < gap < 400:
+                    out.append(b"1" + b" " * max(0, gap - 2))
+                    pos += len(out[-1]) + 1
+            out.append(d)
+            pos += len(d) + 1
+        out.append(ln)
+        pos += len(ln) + 1
+    return b"\n".join(out) + b"\n"

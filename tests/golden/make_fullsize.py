@@ -46,6 +46,7 @@ CONFIGS = {
     "csv_nan_1m_x256": (synth.CSV_NAN, po.CSV, 1 << 20, 256, 0),
     "libsvm_qid_1m_x128": (synth.LIBSVM_QID, po.LIBSVM, 1 << 20, 128, 0),
     "libsvm_cmt_1m_x128": (synth.LIBSVM_CMT, po.LIBSVM, 1 << 20, 128, 0),
+    "libsvm_hdrs_1m_x128": (synth.LIBSVM_HDRS, po.LIBSVM, 1 << 20, 128, 0),
     "libsvm_1b_im1_1m_x128": (synth.LIBSVM_1B, po.LIBSVM, 1 << 20, 128, 0),
     "libfm_1m_x64": (synth.LIBFM, po.LIBFM, 1 << 20, 64, 0),
 }

@@ -625,3 +625,44 @@ def test_emu_exact_gaps_across_segments():
             assert diff(h, o) == [], (it, diff(h, o))
         checked += not failed
     assert checked >= 30, checked
+
+
+def test_emu_fast_dirty_lines_vs_oracle():
+    """Lines holding bytes outside the grammar (svm_fast.h dirty_lines): file
+    headers mid-chunk, words, symbols, inf / nan values, across and near tile
+    ends, with odd chunkings and long dirty lines (the exact kernels' case):
+    the single pass takes the short ones line by line, the rest goes to the
+    exact kernels -- whichever path runs, the reference's result."""
+    rng = np.random.default_rng(3131)
+    paths = {"fast": 0, "exact": 0}
+    for it in range(30):
+        data = fuzz_text.dirty_libsvm(rng, 70000 if it % 3 else 3000, rate=0.01 if it % 2 else 0.05,
+                                      long_frac=0.3 if it % 5 == 4 else 0.0, near_tile_end=it % 3 == 1)
+        offs = fuzz_text.random_cuts(rng, data, 5, anywhere=it % 4 == 3)
+        kw = {"index_bits": 64} if it % 7 == 1 else ({"indexing_mode": -1} if it % 7 == 2 else {})
+        h = _emu_vs_oracle(data, offs, **kw)
+        paths[h["path"]] += 1
+    assert paths["fast"] >= 8 and paths["exact"] >= 3, paths
+
+
+def test_emu_fast_file_headers():
+    """Files with a "# ..." first line concatenated the way InputSplit reads a
+    directory ('\\n' between files, input_split_base.cc:204-210): headers
+    without digitchars are empty lines to the reference and stay on the single
+    pass, also when they sit across a 16 KiB tile end."""
+    rng = np.random.default_rng(909)
+    for it in range(12):
+        files = []
+        for f in range(6):
+            body = fuzz_text.uniform_libsvm(rng, int(rng.integers(50, 400)), 20).replace(b"\r", b"\n")
+            files.append(b"# synth libsvm shard\n" + body.rstrip(b"\n") + b"\n")
+        data = b"\n".join(files) + b"\n"
+        if it % 2:  # move a header across a tile end
+            k = data.index(b"# synth", 16384 - 2000) if len(data) > 20000 else -1
+            if k > 0:
+                pad = 16384 - 10 - k
+                if pad > 0:
+                    data = data[:k - 1] + b" " * pad + data[k - 1:]
+        offs = fuzz_text.random_cuts(rng, data, 4, anywhere=False)
+        h = _emu_vs_oracle(data, offs)
+        assert h["path"] == "fast", it

@@ -344,6 +344,48 @@ def test_gpu_comments_across_tile_ends(dm, body):
                     assert h["path"] == "fast", (d, L)
 
 
+def test_gpu_dirty_lines_vs_oracle(dm):
+    """Per-line fallback (svm_fast.h dirty_lines): lines holding bytes outside
+    the grammar -- file headers mid-chunk, words, symbols, inf / nan values --
+    at several rates, across and near tile ends, with odd chunkings, 64-bit
+    ids and indexing_mode -1, and long dirty lines (the exact kernels' case):
+    the default path and the forced exact path both equal the oracle, and
+    inputs whose dirty lines are all short stay on the single pass."""
+    rng = np.random.default_rng(4242)
+    paths = {"fast": 0, "exact": 0}
+    for it in range(60):
+        data = fuzz_text.dirty_libsvm(rng, 120000 if it % 3 else 5000, rate=(0.002, 0.01, 0.05)[it % 3],
+                                      long_frac=0.3 if it % 5 == 4 else 0.0, near_tile_end=it % 3 == 1)
+        offs = fuzz_text.random_cuts(rng, data, 6, anywhere=it % 4 == 3)
+        kw = {"index_bits": 64} if it % 7 == 1 else ({"indexing_mode": -1} if it % 7 == 2 else {})
+        h = _gpu_vs_oracle_paths(dm, data, offs, **kw)
+        paths[h["path"]] += 1
+    assert paths["fast"] >= 15 and paths["exact"] >= 5, paths
+
+
+def test_gpu_file_headers_stay_on_single_pass(dm):
+    """Files with a "# ..." first line read as a directory by the text
+    InputSplit ('\\n' between files, input_split_base.cc:204-210): every
+    header after the first sits mid-chunk, a line the reference reads (an
+    empty one: no digitchar); headers placed across 16 KiB tile ends at every
+    offset of the last 80 bytes stay on the single pass."""
+    rng = np.random.default_rng(808)
+    for it in range(24):
+        files = []
+        for f in range(5):
+            body = fuzz_text.uniform_libsvm(rng, int(rng.integers(100, 500)), 20).replace(b"\r", b"\n")
+            files.append(b"# synth libsvm shard\n" + body.rstrip(b"\n") + b"\n")
+        data = b"\n".join(files) + b"\n"
+        k = data.find(b"# synth", 16384 - 3000)
+        if 0 < k < 16384:  # this header from 70 bytes before the tile end to 10 after
+            pad = 16384 - 70 + 3 * it - k
+            if pad > 0:
+                data = data[:k - 1] + b" " * pad + data[k - 1:]
+        offs = fuzz_text.random_cuts(rng, data, 4, anywhere=False)
+        h = _gpu_vs_oracle_paths(dm, data, offs, nthread=1 + it % 2)
+        assert h["path"] == "fast", it
+
+
 def test_gpu_comment_bench_size_fast_equals_exact(dm):
     """Config 2 rows, each with a trailing '# row <r>' comment, and a header
     line: single-pass == exact bit for bit (the comment path in every tile)."""

@@ -24,7 +24,8 @@ SLOTS = 16
 def main():
     rows = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 20
     width = int(sys.argv[2]) if len(sys.argv) > 2 else 128
-    kind = {"libsvm": synth.LIBSVM, "qid": synth.LIBSVM_QID, "cmt": synth.LIBSVM_CMT}[
+    kind = {"libsvm": synth.LIBSVM, "qid": synth.LIBSVM_QID, "cmt": synth.LIBSVM_CMT,
+            "hdrs": synth.LIBSVM_HDRS}[
         sys.argv[3] if len(sys.argv) > 3 else "libsvm"]
     dmlc_amd.LIB_PATH = os.path.join(ROOT, "dmlc-core_amd", "lib", "libdmlc_amd_stamps.so")
     L = dmlc_amd.lib()
@@ -67,6 +68,18 @@ def main():
                                  ("  chunk list end", 9, 10), ("  classify barrier", 10, 3)):
                 col = st[:, a1] - st[:, a0]
                 print("  %-18s mean %8.0f cyc  p50 %8.0f" % (name, col.mean(), np.median(col)))
+        if mode == "full":  # the slowest tiles (e.g. the comment / dirty-line pass) and their successors' wait
+            cls = st[:, 3] - st[:, 2]
+            top = np.argsort(cls)[::-1][:6]
+            print("  slowest classify (tile: cycles): %s" % ", ".join("%d: %d" % (k, cls[k]) for k in top))
+            hz = st[:, 12] > st[:, 2]  # tiles that took the comment / dirty-line pass this run
+            if hz.any():
+                for name, a0, a1 in (("comment pass", 2, 12), ("dirty: walk", 12, 13), ("dirty: rest", 13, 14)):
+                    col = (st[:, a1] - st[:, a0])[hz]
+                    print("  %-14s %d tiles mean %8.0f cyc  max %8.0f" % (name, hz.sum(), col.mean(), col.max()))
+            lbk = d[:, 5]
+            print("  look-back p99.9 %.0f max %.0f; tiles with look-back > 40k cycles: %d"
+                  % (np.percentile(lbk, 99.9), lbk.max(), int((lbk > 40000).sum())))
         rounds = st[:, 15]
         print("  look-back rounds: mean %.2f p50 %.0f p99 %.0f max %d"
               % (rounds.mean(), np.median(rounds), np.percentile(rounds, 99), rounds.max()))

@@ -20,6 +20,12 @@
  *    skips the blank before each value, strtonum.h:95-264).
  *  libsvm 1-based row (fmt 6): the libsvm row with every id one higher (no 0
  *    id: indexing_mode=-1 shifts them back, libsvm_parser.h:165-171).
+ *  libsvm directory (fmt 8): the libsvm rows as files of 16384 rows, each
+ *    starting with the header line "# synth libsvm shard", read the way the
+ *    text InputSplit reads a directory -- a '\n' between files
+ *    (input_split_base.cc:204-210), so every header after the first sits
+ *    mid-chunk after an empty line, where the reference parses it as a line
+ *    (libsvm_parser.h:91-104; no digitchar in it: an empty line).
  *  CSV with missing values (fmt 7): the CSV row with 0.1 % of its fields
  *    "nan" (numpy.savetxt's missing value; ParseFloat's NAN branch,
  *    strtonum.h:133-175), and a UTF-8 BOM at the head of the file
@@ -91,7 +97,7 @@ static size_t fmt_csv_row(char *o, uint64_t seed, uint64_t r, int C, int blank, 
 
 /* upper bound on the bytes of `nrows` rows */
 size_t synth_bound(int fmt, uint64_t nrows, int width) {
-  return fmt == 0 || fmt == 3 || fmt == 4 || fmt == 6 ? nrows * (size_t)(2 + 28 + width * 26) + 32
+  return fmt == 0 || fmt == 3 || fmt == 4 || fmt == 6 || fmt == 8 ? nrows * (size_t)(2 + 28 + width * 26) + 32
                   : fmt == 2 ? nrows * (size_t)(2 + width * 30) : nrows * (size_t)(width * 19 + 2) + 3;
 }
 
@@ -115,7 +121,9 @@ size_t synth_rows(int fmt, uint64_t row0, uint64_t nrows, int width, uint64_t se
       if (line_off) line_off[r] = n; /* block-relative; fixed below */
       if (fmt == 4 && row0 + r == 0) n += (size_t)sprintf(buf + n, "# label id:value ... # row r\n");
       if (fmt == 7 && row0 + r == 0) n += (size_t)sprintf(buf + n, "\xEF\xBB\xBF");
-      n += fmt == 0 || fmt == 3 || fmt == 4 || fmt == 6
+      if (fmt == 8 && (row0 + r) % 16384 == 0)
+        n += (size_t)sprintf(buf + n, row0 + r ? "\n# synth libsvm shard\n" : "# synth libsvm shard\n");
+      n += fmt == 0 || fmt == 3 || fmt == 4 || fmt == 6 || fmt == 8
                ? fmt_libsvm_row(buf + n, seed, row0 + r, width, fmt == 3, fmt == 4, fmt == 6)
                     : fmt == 2 ? fmt_libfm_row(buf + n, seed, row0 + r, width)
                                : fmt_csv_row(buf + n, seed, row0 + r, width, fmt == 5, fmt == 7);

@@ -17,6 +17,7 @@ cfg = sys.argv[1] if len(sys.argv) > 1 else "libsvm"
 fmt, rows, width, kind = {"libsvm": ("libsvm", 1 << 20, 128, synth.LIBSVM), "csv": ("csv", 1 << 20, 256, synth.CSV),
                           "qid": ("libsvm", 1 << 20, 128, synth.LIBSVM_QID),
                           "cmt": ("libsvm", 1 << 20, 128, synth.LIBSVM_CMT),
+                          "hdrs": ("libsvm", 1 << 20, 128, synth.LIBSVM_HDRS),
                           "libfm": ("libfm", 1 << 20, 64, synth.LIBFM),
                           "csv_nan": ("csv", 1 << 20, 256, synth.CSV_NAN),
                           "exact": ("libsvm", 1 << 20, 128, synth.LIBSVM),
