@@ -56,15 +56,16 @@ struct LibsvmArgs {
   const uint64_t *qres;
 };
 // windows per exact tile with a count-pass record, and the record bytes
-// (libsvm_core.h); the records are kept only while they stay within about
-// the text's size
+// (libsvm_core.h); the records are kept only while they stay within 5/8 of
+// the text's size + 1 MiB (at the default 256 KiB exact tiles they are 0.55
+// of it; smaller tiles need more per byte and lose them on large inputs)
 DA_HD uint32_t exact_rec_win(uint64_t tile_bytes, uint64_t win_bytes) {
   return (uint32_t)(tile_bytes / win_bytes + 3);
 }
 DA_HD uint64_t exact_rec_bytes(uint64_t ntiles, uint32_t rec_win, int threads) {
   return ntiles * rec_win * ((uint64_t)threads * 16 + 16);
 }
-DA_HD bool exact_rec_on(uint64_t nbytes, uint64_t rec_bytes) { return rec_bytes <= nbytes + (64ull << 20); }
+DA_HD bool exact_rec_on(uint64_t nbytes, uint64_t rec_bytes) { return rec_bytes <= nbytes / 8 * 5 + (1ull << 20); }
 
 // libfm exact tile kernels (libfm_core.h): the libsvm block plus field ids.
 struct LibfmArgs : LibsvmArgs {

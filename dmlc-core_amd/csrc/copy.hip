@@ -125,7 +125,7 @@ extern "C" int dmlc_amd_copy_n_dev(void *const *dst, const void *const *src, con
   const uint64_t per_block = (uint64_t)dmlc_amd::kCopyThreads * dmlc_amd::kCopyUnroll;
   for (int i = 0; i < n; ++i) {
     if (max_bytes[i] == 0) continue;
-    if (!dst[i] || !src[i] || (slot[i] >= 0 && !d_counts)) return DMLC_AMD_ERR_ARG;
+    if (!dst[i] || !src[i] || slot[i] >= DMLC_AMD_COPY_SLOTS || (slot[i] >= 0 && !d_counts)) return DMLC_AMD_ERR_ARG;
     if (((reinterpret_cast<uintptr_t>(dst[i]) | reinterpret_cast<uintptr_t>(src[i])) & 15u) != 0)
       return DMLC_AMD_ERR_ARG;
     const uint64_t nb =

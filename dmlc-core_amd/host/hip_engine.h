@@ -279,22 +279,92 @@ struct PinnedVec {  // page-locked host array, grown on demand (contents not kep
   }
 };
 
+// The same for device arrays, per device: a parser's workers hold a few
+// hundred MB of HBM (text, workspace, CSR outputs); hipMalloc / hipFree of
+// them cost ~10 ms per parser built and ~10 ms per parser destroyed (hipFree
+// synchronises the device), the same order as parsing a 2 GB file
+// (DESIGN.md 5.2).  Up to kDevCacheBytes per device are kept for reuse
+// (HBM is 288 GB per GPU); blocks past that are freed.
+class DevCache {
+ public:
+  static constexpr size_t kDevCacheBytes = size_t(8) << 30;
+  static DevCache &get() {
+    static DevCache *c = new DevCache();  // never destroyed: no HIP call at process exit
+    return *c;
+  }
+  void *take(int dev, size_t bytes, size_t *got) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      auto &fl = free_[dev];
+      auto it = fl.lower_bound(bytes);
+      if (it != fl.end() && it->first <= 2 * bytes) {
+        void *p = it->second;
+        *got = it->first;
+        held_[dev] -= it->first;
+        fl.erase(it);
+        return p;
+      }
+    }
+    void *p = nullptr;
+    hip_check(hipMalloc(&p, bytes), "hipMalloc");
+    *got = bytes;
+    return p;
+  }
+  // false: not kept (the caller frees it)
+  bool give(int dev, void *p, size_t bytes) {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (held_[dev] + bytes > kDevCacheBytes) return false;
+    free_[dev].emplace(bytes, p);
+    held_[dev] += bytes;
+    return true;
+  }
+  // idle non-blocking streams of a device (the calling thread's current one)
+  hipStream_t take_stream(int dev) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      auto &v = streams_[dev];
+      if (!v.empty()) {
+        hipStream_t s = v.back();
+        v.pop_back();
+        return s;
+      }
+    }
+    hipStream_t s = nullptr;
+    hip_check(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
+    return s;
+  }
+  void give_stream(int dev, hipStream_t s) {
+    std::lock_guard<std::mutex> lk(mu_);
+    streams_[dev].push_back(s);
+  }
+
+ private:
+  std::map<int, std::vector<hipStream_t>> streams_;
+  std::mutex mu_;
+  std::map<int, std::multimap<size_t, void *>> free_;
+  std::map<int, size_t> held_;
+};
+
 struct DevBuf {  // device array, grown on demand (contents not kept)
   void *p = nullptr;
   size_t bytes = 0;
+  int dev = -1;  // the device current when it was allocated
   DevBuf() = default;
   DevBuf(const DevBuf &) = delete;
   DevBuf &operator=(const DevBuf &) = delete;
-  ~DevBuf() {
-    if (p) (void)hipFree(p);
+  ~DevBuf() { release(); }
+  void release() {
+    if (p && !DevCache::get().give(dev, p, bytes)) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
   }
   void *get(size_t n) {
     if (n > bytes) {
-      if (p) hip_check(hipFree(p), "hipFree");
-      p = nullptr;
-      const size_t b = n + n / 4 + 256;
-      hip_check(hipMalloc(&p, b), "hipMalloc");
-      bytes = b;
+      release();
+      if (hipGetDevice(&dev) != hipSuccess) throw dmlc::Error("hipGetDevice failed");
+      size_t got = 0;
+      p = DevCache::get().take(dev, n + n / 4 + 256, &got);
+      bytes = got;
     }
     return p;
   }
@@ -417,8 +487,16 @@ class HipTextParser : public dmlc::Parser<IndexType, DType> {
     Start();
   }
   ~HipTextParser() override {
+    const Clock clk;
     Stop();
+    const uint64_t stop_ns = clk.ns();
     if (cfg_.stats) PrintStats();
+    workers_.clear();  // streams and HBM blocks back to DevCache, pinned blocks to PinnedCache
+    pool_.clear();
+    if (cfg_.stats) {
+      std::fprintf(stderr, "{\"dmlc_amd_teardown\": {\"stop_s\": %.4f, \"free_s\": %.4f}}\n", stop_ns * 1e-9,
+                   (clk.ns() - stop_ns) * 1e-9);
+    }
   }
 
   void BeforeFirst() override {
@@ -474,7 +552,8 @@ class HipTextParser : public dmlc::Parser<IndexType, DType> {
         (void)hipSetDevice(device);
         for (auto &e : ev)
           if (e) (void)hipEventDestroy(e);
-        (void)hipStreamDestroy(stream);
+        (void)hipStreamSynchronize(stream);  // (idle: each batch ends with a sync)
+        DevCache::get().give_stream(device, stream);
         if (have_prev && prev != device) (void)hipSetDevice(prev);
       }
     }
@@ -606,7 +685,7 @@ class HipTextParser : public dmlc::Parser<IndexType, DType> {
       try {
         if (!ready) {
           hip_check(hipSetDevice(w->device), "hipSetDevice");
-          if (!w->stream) hip_check(hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking), "hipStreamCreate");
+          if (!w->stream) w->stream = DevCache::get().take_stream(w->device);
           ready = true;
         }
         if (b->nchunks > 0) Parse(w, b);
@@ -687,6 +766,9 @@ class HipTextParser : public dmlc::Parser<IndexType, DType> {
       Outputs(w, want, &out);
       CheckRc(dmlc_amd_parse(d_text, b->bytes, d_cs, nch, &p, &out, d_tab, d_ws, ws,
                              reinterpret_cast<dmlc_amd_result *>(d_res), s));
+      // stats: the parse / D2H boundary right after the parse (the queued
+      // copy-out and the result block count as D2H)
+      if (st) hip_check(hipEventRecord(w->ev[2], s), "hipEventRecord");
       pre = attempt == 0 && cfg_.precopy && cfg_.d2h_kernel() && w->est[0] > 0;
       if (pre) {
         const void *src[8] = {out.offset, out.label, out.weight, out.qid, out.index, out.field, out.value, d_tab};
@@ -703,7 +785,6 @@ class HipTextParser : public dmlc::Parser<IndexType, DType> {
         CheckRc(dmlc_amd_copy_n_dev(pre_dst, src, d_res, kSlot, kScale, kAdd, pre_max, 8, s));
       }
       hip_check(hipMemcpyAsync(hres, d_res, sizeof(dmlc_amd_result), hipMemcpyDeviceToHost, s), "D2H result");
-      if (st) hip_check(hipEventRecord(w->ev[2], s), "hipEventRecord");
       hip_check(hipStreamSynchronize(s), "hipStreamSynchronize");
       if ((hres->error & 0xFFFF) != DMLC_AMD_ERR_CAPACITY) break;
       if (attempt > 0) throw dmlc::Error("dmlc_amd_parse: output capacity exceeded at exact sizes");

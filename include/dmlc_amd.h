@@ -156,9 +156,12 @@ int dmlc_amd_copy_n(void *const *dst, const void *const *src, const uint64_t *by
 /* The same with sizes known only on the device (a parse's result counts, so
  * the copy-out needs no host round trip after the parse): copy i moves
  * min(max_bytes[i], d_counts[slot[i]] * scale[i] + add[i]) bytes, or add[i]
- * when slot[i] < 0.  d_counts is read on the device when the copy runs;
- * slot / scale / add / max_bytes are host arrays of n entries.  All pairs
- * must be 16-byte aligned. */
+ * when slot[i] < 0.  d_counts is read on the device when the copy runs: it
+ * holds DMLC_AMD_COPY_SLOTS words (dmlc_amd_result.count), so slot[i] >=
+ * DMLC_AMD_COPY_SLOTS is rejected (DMLC_AMD_ERR_ARG); slot / scale / add /
+ * max_bytes are host arrays of n entries.  All pairs must be 16-byte
+ * aligned. */
+#define DMLC_AMD_COPY_SLOTS 8
 int dmlc_amd_copy_n_dev(void *const *dst, const void *const *src, const uint64_t *d_counts, const int *slot,
                         const uint64_t *scale, const uint64_t *add, const uint64_t *max_bytes, int n,
                         void *stream);

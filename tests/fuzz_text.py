@@ -461,3 +461,66 @@ def dirty_libsvm(rng, nbytes, rate=0.002, long_frac=0.0, near_tile_end=False):
         out.append(ln)
         pos += len(ln) + 1
     return b"\n".join(out) + b"\n"
+
+
+def long_row_libsvm(rng, form, row_kb=(34, 70)):
+    """Short rows around one to three rows longer than four exact windows
+    (> 32 KiB), so that at exact tile_bytes=4096 (three recorded windows per
+    tile, args.h exact_rec_win) a row crosses tile ends past the count pass's
+    records (libsvm_core.h: the write pass restores the role state and the
+    pending token from rec_meta there).  form: "valued" (every pair has a
+    value), "mid_pair" (the long row ends with an index and ':' missing),
+    "dangling" (it ends with "idx:"), "long_head" (labels / values of up to
+    ~300 digits, so tokens straddle window edges), "index_only" (no values)."""
+    def tok(i):
+        if form == "index_only":
+            return "%d" % i
+        if form == "long_head" and rng.random() < 0.02:
+            return "%d:0.%s" % (i, "".join(rng.choice(list("0123456789"), int(rng.integers(50, 300)))))
+        return "%d:%.6g" % (i, rng.random())
+    def label():
+        if form == "long_head" and rng.random() < 0.3:
+            return "1." + "0" * int(rng.integers(100, 400)) + "1"
+        return str(int(rng.integers(0, 2)))
+    rows = []
+    nlong = int(rng.integers(1, 4))
+    where = sorted(rng.choice(np.arange(1, 40), nlong, replace=False).tolist())
+    for r in range(40):
+        if r in where:
+            target = int(rng.integers(row_kb[0], row_kb[1])) << 10
+            parts, n, i = [label()], 0, 0
+            while n < target:
+                i += int(rng.integers(1, 5))
+                t = tok(i)
+                parts.append(" " * int(rng.integers(1, 3)) + t)
+                n += len(t) + 2
+            if r == where[-1] and form == "mid_pair":
+                parts.append(" %d" % (i + 1))
+            elif r == where[-1] and form == "dangling":
+                parts.append(" %d:" % (i + 1))
+            rows.append("".join(parts))
+        else:
+            rows.append(" ".join([label()] + [tok(j) for j in range(int(rng.integers(0, 12)))]))
+    pad = " " * int(rng.integers(0, 8192))  # moves the rows against the 4 KiB tiles and 8 KiB windows
+    return (pad + "\n".join(rows) + "\n").encode()
+
+
+def wide_row_csv(rng, row_kb=(34, 70)):
+    """CSV rows with one to three rows wider than four exact windows (the
+    CSV write pass recounts past its records, csv_core.h)."""
+    rows = []
+    ncol = None
+    nlong = int(rng.integers(1, 4))
+    where = set(rng.choice(np.arange(0, 30), nlong, replace=False).tolist())
+    for r in range(30):
+        if r in where:
+            target = int(rng.integers(row_kb[0], row_kb[1])) << 10
+            f, n = [], 0
+            while n < target:
+                x = "%.5g" % (rng.random() * 100) if rng.random() < 0.8 else ""
+                f.append(x)
+                n += len(x) + 1
+            rows.append(",".join(f))
+        else:
+            rows.append(",".join("%.4g" % rng.random() for _ in range(int(rng.integers(1, 20)))))
+    return ("\n".join(rows) + "\n").encode()

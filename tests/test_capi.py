@@ -64,6 +64,14 @@ def test_workspace_and_argument_validation(lib):
     assert 0 < wf < (1 << 30) // tile * 64 + (1 << 20)  # (no records for libfm)
     small = dmlc_amd.make_params("libsvm", tile_bytes=64)  # tiny exact tiles: records off
     assert dmlc_amd.lib().dmlc_amd_workspace_bytes(1 << 30, 128, ctypes.byref(small)) < (1 << 30) * 2
+    # records never exceed 5/8 of the text + 1 MiB (args.h exact_rec_on), whatever the exact tile
+    for tb in (4096, 9000, 65536, 1 << 18, 1 << 20):
+        q = dmlc_amd.make_params("libsvm", tile_bytes=tb)
+        for n in (1 << 16, 1 << 20, 32 << 20, 1 << 30):
+            base = dmlc_amd.make_params("libfm", tile_bytes=tb)  # the same tables without records
+            extra = (dmlc_amd.lib().dmlc_amd_workspace_bytes(n, 128, ctypes.byref(q))
+                     - dmlc_amd.lib().dmlc_amd_workspace_bytes(n, 128, ctypes.byref(base)))
+            assert extra <= n // 8 * 5 + (1 << 20) + 4096, (tb, n, extra)
     # bad index_bits is rejected before any device work
     bad = dmlc_amd.make_params("libsvm", index_bits=16)
     csr = dmlc_amd.Csr()
@@ -75,6 +83,25 @@ def test_workspace_and_argument_validation(lib):
     rc = dmlc_amd.lib().dmlc_amd_parse(None, 0, None, 0, ctypes.byref(c), ctypes.byref(csr), None,
                                       None, 0, None, None)
     assert rc == 32
+
+
+def test_copy_n_dev_rejects_slot_past_the_counts(lib):
+    """dmlc_amd_copy_n_dev reads d_counts[slot] on the device: slots past the
+    DMLC_AMD_COPY_SLOTS words of dmlc_amd_result.count are refused before any
+    launch (so no GPU is needed)."""
+    f = lib.dmlc_amd_copy_n_dev
+    f.restype = ctypes.c_int
+    P = ctypes.c_void_p
+    dst = (P * 1)(16)
+    src = (P * 1)(32)
+    cnt = (ctypes.c_uint64 * 8)()
+    one = (ctypes.c_uint64 * 1)(1)
+    big = (ctypes.c_uint64 * 1)(64)
+    zero = (ctypes.c_uint64 * 1)(0)
+    for s in (8, 9, 1 << 20):
+        sl = (ctypes.c_int * 1)(s)
+        assert f(dst, src, cnt, sl, one, zero, big, 1, None) == 32, s
+    assert f(dst, src, cnt, (ctypes.c_int * 1)(0), one, zero, big, 17, None) == 32  # n > DMLC_AMD_COPY_MAX
 
 
 def test_device_count_without_gpu(lib):

@@ -666,3 +666,36 @@ def test_emu_fast_file_headers():
         offs = fuzz_text.random_cuts(rng, data, 4, anywhere=False)
         h = _emu_vs_oracle(data, offs)
         assert h["path"] == "fast", it
+
+
+@pytest.mark.parametrize("form", ["valued", "mid_pair", "dangling", "long_head", "index_only"])
+def test_emu_exact_rows_past_the_records(form):
+    """Rows over 32 KiB crossing exact tile ends at tile_bytes=4096: the
+    write pass runs past the count pass's three recorded windows per tile and
+    restores the role state and pending token from rec_meta
+    (libsvm_core.h:406) -- equal to the oracle."""
+    rng = np.random.default_rng({"valued": 1, "mid_pair": 2, "dangling": 3, "long_head": 4, "index_only": 5}[form])
+    for it in range(3):
+        data = fuzz_text.long_row_libsvm(rng, form)
+        offs = fuzz_text.random_cuts(rng, data, 2, anywhere=False)
+        o = po.parse_chunks(data, offs, fmt=po.LIBSVM)
+        h = pyemu.parse(data, offs, "libsvm", exact=True, tile_bytes=4096)
+        failed = check_fail(h, "libsvm", offs)
+        assert (o["status"] != 0) == failed, (form, it, o["msg"], h["error"])
+        if not failed:
+            assert diff(h, o) == [], (form, it, diff(h, o))
+
+
+def test_emu_csv_exact_wide_rows_past_the_records():
+    """The CSV write pass recounts windows past its records (csv_core.h:451):
+    rows over 32 KiB at tile_bytes=4096 equal the oracle."""
+    rng = np.random.default_rng(77)
+    for it in range(4):
+        data = fuzz_text.wide_row_csv(rng)
+        offs = fuzz_text.random_cuts(rng, data, 2, anywhere=False)
+        o = po.parse_chunks(data, offs, fmt=po.CSV)
+        h = pyemu.parse(data, offs, "csv", exact=True, tile_bytes=4096)
+        failed = check_fail(h, "csv", offs)
+        assert (o["status"] != 0) == failed, (it, o["msg"], h["error"])
+        if not failed:
+            assert diff(h, o) == [], (it, diff(h, o))

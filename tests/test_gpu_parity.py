@@ -149,6 +149,28 @@ def test_gpu_long_lines_vs_oracle(dm):
     _oracle_vs_gpu(dm, csvl.encode(), [0, len(csvl)], po.CSV, tile_bytes=4096)
 
 
+@pytest.mark.parametrize("form", ["valued", "mid_pair", "dangling", "long_head", "index_only"])
+def test_gpu_exact_rows_past_the_records(dm, form):
+    """Rows over 32 KiB crossing exact tile ends at tile_bytes=4096: the write
+    pass runs past the count pass's three recorded windows per tile and
+    restores the role state and pending token from rec_meta
+    (libsvm_core.h:406); rows ending mid-pair / with "idx:" / long heads."""
+    rng = np.random.default_rng(500 + ["valued", "mid_pair", "dangling", "long_head", "index_only"].index(form))
+    for it in range(6):
+        data = fuzz_text.long_row_libsvm(rng, form)
+        h = _oracle_vs_gpu(dm, data, fuzz_text.random_cuts(rng, data, 2), po.LIBSVM, exact=True, tile_bytes=4096)
+        assert h["path"] == "exact"
+
+
+def test_gpu_csv_exact_wide_rows_past_the_records(dm):
+    """The CSV write pass recounts windows past its records (csv_core.h:451)."""
+    rng = np.random.default_rng(577)
+    for it in range(8):
+        data = fuzz_text.wide_row_csv(rng)
+        h = _oracle_vs_gpu(dm, data, fuzz_text.random_cuts(rng, data, 2), po.CSV, exact=True, tile_bytes=4096)
+        assert h["path"] == "exact"
+
+
 def _fuzz_text(rng, fmt):
     alpha = {po.LIBSVM: list("0123456789") * 6 + list("  ::.-+eE#\tq") + ["qid:", "nan", "inf", "\r"],
              po.CSV: list("0123456789") * 6 + list(",,,,.-+eE \t") + ["nan", "inf", "0x", "\xef\xbb\xbf"],

@@ -391,19 +391,25 @@ def test_api_multi_device_dispatch(tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", ["kernel", "dma"])
-def test_api_copy_modes(tmp_path, mode):
-    """DMLC_AMD_COPY: the batch's CSR arrays copied out by one copy kernel
-    (kernel, the default) or one DMA per array (dma) -- both modes' blocks
-    equal the oracle's parse, over many
-    batches, with weights and qids and a CSV / libfm file."""
+@pytest.mark.parametrize("mode,precopy", [("d2h_kernel", 1), ("d2h_kernel", 0), ("kernel", 1), ("h2d_kernel", 1),
+                                          ("dma", 1)])
+def test_api_copy_modes(tmp_path, mode, precopy):
+    """DMLC_AMD_COPY: the text in and the batch's CSR arrays out by copy
+    kernels (kernel), by DMA (dma), or one direction each (d2h_kernel, the
+    default: the copy-out by one kernel queued behind the parse with sizes
+    read on the device; h2d_kernel); DMLC_AMD_PRECOPY=0 waits for the parse's
+    counts before copying out.  Every mode's blocks equal the oracle's parse,
+    over many batches, with weights and qids, a CSV / libfm file, and a file
+    whose later batches hold far more entries per byte than the first (the
+    queued copy-out's size estimate is exceeded and the batch copies again,
+    hip_engine.h `again`)."""
     text, _ = synth.rows(synth.LIBSVM, 30000, 48, seed=21)
     lines = text.tobytes().split(b"\n")
     for i in range(0, len(lines) - 1):  # label:weight and qid on every row (a RowBlock reader takes `size`)
         head, _, rest = lines[i].partition(b" ")
         lines[i] = head + b":0.%d qid:%d " % (1 + i % 9, i // 3) + rest
     svm = b"\n".join(lines)
-    env = {"DMLC_AMD_COPY": mode, "DMLC_AMD_BATCH_BYTES": str(1 << 20)}
+    env = {"DMLC_AMD_COPY": mode, "DMLC_AMD_BATCH_BYTES": str(1 << 20), "DMLC_AMD_PRECOPY": str(precopy)}
     d, _ = _write(tmp_path / "svm", [svm])
     o, _ = oracle_files([svm])
     h = run_api(tmp_path, d, env=env)
@@ -416,6 +422,16 @@ def test_api_copy_modes(tmp_path, mode):
         oo, _ = oracle_files([t.tobytes()], fmt=pfmt)
         hh = run_api(tmp_path, dd, fmt=name, env=env)
         assert "error" not in hh and diff(hh, oo) == [], (mode, name)
+    # long-valued rows first (~20 bytes per entry), then dense short ones (~4)
+    rng = np.random.default_rng(23)
+    grow = b"".join(b"1 " + b" ".join(b"%d:%.12f" % (j, rng.random()) for j in range(40)) + b"\n"
+                    for _ in range(4000))
+    grow += b"".join(b"0 " + b" ".join(b"%d:1" % j for j in range(1, 60)) + b"\n" for _ in range(12000))
+    dg, _ = _write(tmp_path / "grow", [grow])
+    og, _ = oracle_files([grow])
+    hg = run_api(tmp_path, dg, env=env)
+    assert "error" not in hg and diff(hg, og) == [], (mode, "grow")
+    assert hg["blocks"].tolist() == og["blocks"]["rows"].tolist(), mode
 
 
 @pytest.mark.gpu

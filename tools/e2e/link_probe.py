@@ -17,7 +17,7 @@ import dmlc_amd  # noqa: E402
 
 
 def main():
-    n = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 30
+    n = int(sys.argv[1]) if len(sys.argv) > 1 and int(sys.argv[1]) > 0 else 1 << 30
     L = dmlc_amd.lib()
     host_in = torch.empty(n, dtype=torch.uint8).pin_memory()
     host_out = torch.empty(n, dtype=torch.uint8).pin_memory()
@@ -108,7 +108,62 @@ def host_memcpy(n=1 << 30, threads=(1, 4, 8, 16)):
         print(json.dumps({"case": "host_memcpy", "threads": t, "GBps_rw": round(2 * n / best / 1e9, 1)}), flush=True)
 
 
+def sweep(sizes_mib=(4, 16, 64, 256, 1024), total=2 << 30):
+    """Copy-size sweep: per copy size, direction, engine
+    (copy kernel / DMA) and stream count (one stream; two streams taking
+    alternate copies), back-to-back copies moving `total` bytes, timed from
+    the first enqueue to the sync: the rate a pipeline of that batch size can
+    get from the link.  Also both directions at once (two streams, one per
+    direction) per size."""
+    L = dmlc_amd.lib()
+    big = max(sizes_mib) << 20
+    host = [torch.empty(big, dtype=torch.uint8).pin_memory() for _ in range(2)]
+    dev = [torch.ones(big, dtype=torch.uint8, device="cuda") for _ in range(2)]
+    ss = [torch.cuda.Stream(), torch.cuda.Stream()]
+
+    def one(eng, dst, src, nb, s):
+        if eng == "kernel":
+            assert L.dmlc_amd_copy(dst.data_ptr(), src.data_ptr(), nb, s.cuda_stream) == 0
+        else:
+            with torch.cuda.stream(s):
+                dst[:nb].copy_(src[:nb], non_blocking=True)
+
+    for mib in sizes_mib:
+        nb = mib << 20
+        reps = max(2, total // nb)
+        for eng in ("kernel", "dma"):
+            for direction in ("h2d", "d2h", "both"):
+                for nstream in ((1, 2) if direction != "both" else (2,)):
+                    best = 1e30
+                    for _ in range(2):
+                        torch.cuda.synchronize()
+                        t0 = time.perf_counter()
+                        for r in range(reps):
+                            w = r % nstream
+                            if direction == "both":
+                                one(eng, dev[0], host[0], nb, ss[0])
+                                one(eng, host[1], dev[1], nb, ss[1])
+                            elif direction == "h2d":
+                                one(eng, dev[w], host[w], nb, ss[w])
+                            else:
+                                one(eng, host[w], dev[w], nb, ss[w])
+                        torch.cuda.synchronize()
+                        best = min(best, time.perf_counter() - t0)
+                    moved = nb * reps * (2 if direction == "both" else 1)
+                    print(json.dumps({"case": "sweep", "copy_mib": mib, "engine": eng, "dir": direction,
+                                      "streams": nstream, "copies": reps * (2 if direction == "both" else 1),
+                                      "GBps": round(moved / best / 1e9, 2)}), flush=True)
+
+
 if __name__ == "__main__":
-    main()
-    batched()
-    host_memcpy()
+    what = sys.argv[2:] or ["main", "batched", "host"]
+    if "main" in what:
+        main()
+    if "batched" in what:
+        batched()
+        for nb in (4 << 20, 16 << 20, 64 << 20, 256 << 20):
+            batched(nb=nb, reps=max(8, (1 << 30) // nb))
+    if "sweep" in what:
+        sweep()
+    if "host" in what:
+        host_memcpy()

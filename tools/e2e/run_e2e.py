@@ -42,6 +42,8 @@ def main():
                             env=dict(os.environ, DMLC_AMD_STATS="1"))  # stats of the last (warm) pass
         st = [json.loads(x) for x in r2.stderr.splitlines() if x.startswith('{"dmlc_amd_stats"')]
         line["stages"] = st[-1]["dmlc_amd_stats"] if st else None
+        td = [json.loads(x) for x in r2.stderr.splitlines() if x.startswith('{"dmlc_amd_teardown"')]
+        line["teardown"] = td[-1]["dmlc_amd_teardown"] if td else None
         line["stages_pass_s"] = json.loads(r2.stdout)["best_s"] if r2.returncode == 0 else None
         line["cpu_reference"] = None
         try:
