@@ -44,7 +44,7 @@ constexpr uint32_t kSpinLimit = 1u << 22;
 // of each tile records s_memtime at phase boundaries into g_stamps; the
 // product build executes no stamp.
 constexpr uint32_t kStampTiles = 1u << 17;
-constexpr uint32_t kStampSlots = 16;  // per tile: 0 realtime start, 1.. phase ends, 15 look-back rounds
+constexpr uint32_t kStampSlots = 20;  // per tile: 0 realtime start, 1.. phase ends, 15 look-back rounds
 #if defined(DMLC_AMD_STAMPS) && defined(__HIPCC__)
 __device__ uint64_t g_stamps[kStampTiles * kStampSlots];
 #endif

@@ -615,8 +615,34 @@ DA_HD SegOut segment_roles(const Tile &t, int tid) {
     if (cq && (P + 64 >= a.n || t.is_cs(P + 64))) o.bad = 1;
     Q = RS & t3 & ~L;
     if (Q & K) o.bad = 1;  // a ':' and a token in one gap ("l : qid:5" pairs l with 5)
-    for (uint64_t m = Q; m; m &= m - 1)
-      if (!t.qid_ok(P + ctz64(m))) o.bad = 1;
+    if (Q) {
+      // qid_ok from the planes where the run before the token is the line's
+      // label (role L: only blanks and the token between them, the common
+      // "label qid:n" form): the value is 1-18 plain digits ending at a
+      // non-digitchar -- the digitchar run at x and its G (digit) bits, read
+      // as 128-bit windows over this segment and the next.  After a weight,
+      // or near the tile's end, the byte walk (Tile::qid_ok).
+      const uint64_t Zq = ~RS, xlq = L << 1;
+      const uint64_t afterL = ((Zq + (xlq & Zq) + (prole == R_L ? 1u : 0u)) | xlq) & RS;
+      uint64_t slow = Q & ~afterL;
+      const bool lastseg = tid + 1 >= kFThreads;
+      const uint64_t Dn = lastseg ? 0 : t.sh->u.m.d[tid + 2];
+      const uint64_t Gc = t.sh->gw[2 * tid] | ((uint64_t)t.sh->gw[2 * tid + 1] << 32);
+      const uint64_t Gn = lastseg ? 0 : t.sh->gw[2 * tid + 2] | ((uint64_t)t.sh->gw[2 * tid + 3] << 32);
+      for (uint64_t m = Q & afterL; m; m &= m - 1) {
+        const uint32_t b = ctz64(m);
+        if (lastseg && b + 19 > 64) {
+          slow |= 1ull << b;
+          continue;
+        }
+        const uint64_t r = b ? (D >> b) | (Dn << (64 - b)) : D;
+        const uint64_t g = b ? (Gc >> b) | (Gn << (64 - b)) : Gc;
+        const uint32_t len = ~r ? (uint32_t)ctz64(~r) : 64u;  // >= 1: a run starts at b
+        if (len > 18 || (~g & ((1ull << len) - 1))) o.bad = 1;
+      }
+      for (uint64_t m = slow; m; m &= m - 1)
+        if (!t.qid_ok(P + ctz64(m))) o.bad = 1;
+    }
   }
   const uint64_t Z = ~RS;
   const uint64_t xl = L << 1, xk = K << 1, xq = Q << 1;
@@ -1285,7 +1311,8 @@ DA_HDF uint32_t dirty_lines(const Tile &t, Shared &sh, uint32_t bad, BK &bk, At 
 // (inline: out of line, the call frame's spills cost the kernel 2.2x, 3.97 ms
 // on config 2)
 template <class BK>
-DA_HDF uint32_t comments_reclassify(const Tile t, Shared &sh, uint32_t bad0, BK &bk) {
+DA_HDF uint32_t comments_reclassify(const Tile t, Shared &sh, uint32_t bad0, BK &bk, uint32_t k) {
+  (void)k;  // (phase stamps of the diagnostic build)
   const int tid = bk.tid();
   const FastSvmArgs &a = *t.a;
   const uint32_t e = comment_erase(t.tlo, t.thi, a.n, sh.c, &sh.hashy, bk, sh.u.m.d[tid + 1], sh.u.m.n[tid + 1],
@@ -1296,6 +1323,7 @@ DA_HDF uint32_t comments_reclassify(const Tile t, Shared &sh, uint32_t bad0, BK 
     sh.prebad = 0;
   }
   bk.sync();
+  FAST_STAMP(k, 16);
   auto at = [&](uint64_t p) -> uint32_t {
     if (p >= a.n) return 0u;
     return p + kPre >= t.tlo ? (uint32_t)sh.c.text[p - t.tlo + kPre] : gbyte(a.text, p);
@@ -1425,7 +1453,7 @@ DA_HDF uint32_t tile_p(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k, Sta
       }
       bk.sync();
     }
-    if (sh.nseg > 2u || sh.dgate) bad = comments_reclassify(t, sh, bad, bk);
+    if (sh.nseg > 2u || sh.dgate) bad = comments_reclassify(t, sh, bad, bk, k);
     FAST_STAMP(k, 12);
     bad = dirty_lines(t, sh, bad, bk, at, k);  // lines still holding bytes outside the grammar
     FAST_STAMP(k, 14);

@@ -18,7 +18,7 @@ import dmlc_amd  # noqa: E402
 from tools import synth  # noqa: E402
 
 PHASES = ["stage", "classify", "roles+scan", "lists", "batch decode", "look-back", "stores"]
-SLOTS = 16
+SLOTS = 20  # fast_common.h kStampSlots
 
 
 def main():
@@ -74,9 +74,13 @@ def main():
             print("  slowest classify (tile: cycles): %s" % ", ".join("%d: %d" % (k, cls[k]) for k in top))
             hz = st[:, 12] > st[:, 2]  # tiles that took the comment / dirty-line pass this run
             if hz.any():
-                for name, a0, a1 in (("comment pass", 2, 12), ("dirty: walk", 12, 13), ("dirty: rest", 13, 14)):
-                    col = (st[:, a1] - st[:, a0])[hz]
-                    print("  %-14s %d tiles mean %8.0f cyc  max %8.0f" % (name, hz.sum(), col.mean(), col.max()))
+                for name, a0, a1 in (("comment pass", 2, 12), ("  erase", 10, 16), ("  reclassify", 16, 12),
+                                     ("dirty: walk", 12, 13), ("dirty: rest", 13, 14)):
+                    sel = hz & (st[:, a1] > 0) & (st[:, a0] > 0)
+                    if not sel.any():
+                        continue
+                    col = (st[:, a1] - st[:, a0])[sel]
+                    print("  %-14s %d tiles mean %8.0f cyc  max %8.0f" % (name, sel.sum(), col.mean(), col.max()))
             lbk = d[:, 5]
             print("  look-back p99.9 %.0f max %.0f; tiles with look-back > 40k cycles: %d"
                   % (np.percentile(lbk, 99.9), lbk.max(), int((lbk > 40000).sum())))
