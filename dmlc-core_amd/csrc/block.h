@@ -36,6 +36,14 @@ struct DevBlockT {
     __builtin_amdgcn_wave_barrier();
   }
 
+  // one word per wave (its lane 0's) for the whole block: wave_put, the
+  // caller's sync(), then wave_get(w) in any thread (the scan scratch: no scan
+  // may run between the put and the last get without a sync in between)
+  __device__ __forceinline__ void wave_put(uint32_t v) const {
+    if ((threadIdx.x & (kWave - 1)) == 0) scratch[threadIdx.x / kWave] = v;
+  }
+  __device__ __forceinline__ uint32_t wave_get(int w) const { return (uint32_t)scratch[w]; }
+
   // v of lane `src` of the calling wave (all lanes active)
   template <typename T>
   __device__ __forceinline__ static T shfl(T v, int src) {

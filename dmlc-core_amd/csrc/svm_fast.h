@@ -469,16 +469,17 @@ DA_HD uint64_t cs_bits(const TileCommon &c, uint64_t lo) {
 // every wave through the slowest lane's segment.
 template <class BK>
 DA_HDF uint32_t comment_erase(uint64_t tlo, uint64_t thi, uint64_t n, TileCommon &c, uint32_t *note, BK &bk,
-                              uint64_t D, uint64_t N, uint64_t C, bool raw) {
+                              uint64_t D, uint64_t N, uint64_t C, bool raw, uint32_t k) {
+  (void)k;  // (phase stamps of the diagnostic build)
   const int tid = bk.tid();
   const uint32_t lane = (uint32_t)tid & (kWave - 1), wbase = (uint32_t)tid - lane;
   uint8_t *txt = c.text;
   const uint64_t P = tlo + (uint64_t)tid * kSegB;
-  CmtMasks k = plane_cmt_masks(D, N, C);
+  CmtMasks km = plane_cmt_masks(D, N, C);
   for (uint64_t m = bk.ballot(raw); m; m &= m - 1) {  // wave-uniform
     const uint32_t s = (uint32_t)ctz64(m);
     const CmtMasks kk = wave_cmt_masks(txt + kPre + (wbase + s) * kSegB, bk);
-    if (lane == s) k = kk;
+    if (lane == s) km = kk;
   }
   // wave 0: the pre-halo's masks; wave 3: the post-halo's
   CmtMasks kh{0, 0, 0, 0}, kp[kPost / kSegB];
@@ -497,20 +498,62 @@ DA_HDF uint32_t comment_erase(uint64_t tlo, uint64_t thi, uint64_t n, TileCommon
     const uint32_t c0 = comment_fn(hA, hB) & 1u;
     *note = 1u | (r0 << 1) | (c0 << 2);  // (stays nonzero: the caller's branch read it)
   }
-  uint32_t tot;
-  const uint32_t rpre = bk.exclusive(reach_fn(k, S), 2u, CommentFnCompose(), &tot);
-  const uint32_t r = (rpre >> ((*note >> 1) & 1u)) & 1u;
+  FAST_STAMP(k, 17);
+  // The reach and comment state at each segment start, one barrier.  Both
+  // per-segment maps (reach-in -> reach-out, open-in -> open-after) are
+  // monotone: constant 0 (0b00), constant 1 (0b11) or the identity (0b10)
+  // (add_carry's carry-out never falls when the carry-in rises), so a
+  // segment's state is the constant of the nearest non-identity segment
+  // before it, else the tile start's (*note).  In-wave by ballots; across
+  // waves each wave publishes its reach map and its comment map for either
+  // reach-in at its start (its leading segments' reach depends on it).
+  const uint32_t fr = reach_fn(km, S);
+  uint32_t fc0, fc1;
+  {
+    uint64_t A0, B0, A1, B1;
+    comment_ab(km, S, 0u, &A0, &B0);
+    comment_ab(km, S, 1u, &A1, &B1);
+    fc0 = comment_fn(A0, B0);
+    fc1 = comment_fn(A1, B1);
+  }
+  const uint64_t below = (1ull << lane) - 1;
+  // the value at the lane's start from the wave's non-identity maps (nim) and
+  // their constants (one): -1 when none lies before the lane
+  auto anchor = [&](uint64_t nim, uint64_t one) -> int {
+    const uint64_t b = nim & below;
+    return b ? (int)((one >> (63 - clz64(b))) & 1u) : -1;
+  };
+  auto wave_map = [](uint64_t nim, uint64_t one) -> uint32_t {  // the wave's composed map
+    return nim ? (((one >> (63 - clz64(nim))) & 1u) ? 3u : 0u) : 2u;
+  };
+  const uint64_t rn = bk.ballot(fr != 2u), r1 = bk.ballot(fr == 3u);
+  const int ra = anchor(rn, r1);
+  // the lane's comment map for wave reach-in 0 / 1
+  const uint32_t g0 = ra >= 0 ? (ra ? fc1 : fc0) : fc0, g1 = ra >= 0 ? (ra ? fc1 : fc0) : fc1;
+  const uint64_t cn0 = bk.ballot(g0 != 2u), c10 = bk.ballot(g0 == 3u);
+  const uint64_t cn1 = bk.ballot(g1 != 2u), c11 = bk.ballot(g1 == 3u);
+  const uint32_t wid = (uint32_t)tid / kWave;
+  bk.wave_put(wave_map(rn, r1) | (wave_map(cn0, c10) << 2) | (wave_map(cn1, c11) << 4));
+  bk.sync();
+  uint32_t rw = (*note >> 1) & 1u, cw = (*note >> 2) & 1u;  // the tile start's reach / open state
+  for (uint32_t w = 0; w < wid; ++w) {
+    const uint32_t m = bk.wave_get((int)w);
+    cw = (m >> (rw ? 4 : 2) >> cw) & 1u;  // the wave's comment map for its reach-in, applied
+    rw = (m >> rw) & 1u;
+  }
+  FAST_STAMP(k, 18);
+  const uint32_t r = ra >= 0 ? (uint32_t)ra : rw;
+  const int ca = rw ? anchor(cn1, c11) : anchor(cn0, c10);
+  const uint32_t cin = ca >= 0 ? (uint32_t)ca : cw;
   uint64_t A, B;
-  comment_ab(k, S, r, &A, &B);
-  const uint32_t f = comment_fn(A, B);
+  comment_ab(km, S, r, &A, &B);
   uint32_t f_next = 0;  // the next tile's reading of its pre-halo (this segment)
   if (tid == kFThreads - 1) {
     uint64_t An, Bn;
-    comment_ab(k, S, 0u, &An, &Bn);
+    comment_ab(km, S, 0u, &An, &Bn);
     f_next = comment_fn(An, Bn) & 1u;
   }
-  const uint32_t pre = bk.exclusive(f, 2u, CommentFnCompose(), &tot);
-  const uint32_t cin = (pre >> ((*note >> 2) & 1u)) & 1u;
+  FAST_STAMP(k, 19);
   uint32_t co, gate = 0;
   const uint64_t M = comment_mask(A, B, cin, &co);
   for (uint64_t m = bk.ballot(M != 0); m; m &= m - 1) {  // wave-uniform
@@ -529,7 +572,7 @@ DA_HDF uint32_t comment_erase(uint64_t tlo, uint64_t thi, uint64_t n, TileCommon
     if (tid == kFThreads - 1) {
       if (thi < n && P + kSegB == thi && !(cs_bits(c, thi) & 1u) && co != f_next) gate = 1;
       uint32_t ci = co, ri;
-      (void)reach_of(k, S, r, &ri);
+      (void)reach_of(km, S, r, &ri);
       for (int s = 0; s < kPost / kSegB; ++s) {
         const uint64_t Sp = cs_bits(c, tlo + kTile + (uint64_t)s * kSegB);
         uint64_t Ap, Bp;
@@ -903,6 +946,7 @@ DA_HDF uint32_t commit_seg(const Tile &t, Shared &sh, int seg, At at, bool first
   sh.u.m.c[seg + 1] = m.c;
   bad |= m.bad;
   if (!FM && first && m.bad) sh.hashy = 1;
+  if (!FM && first && (m.g & ~m.d)) atomic_add_u32(&sh.nseg, 1u);  // segments holding bytes outside the grammar
   return bad;
 }
 
@@ -1316,7 +1360,7 @@ DA_HDF uint32_t comments_reclassify(const Tile t, Shared &sh, uint32_t bad0, BK 
   const int tid = bk.tid();
   const FastSvmArgs &a = *t.a;
   const uint32_t e = comment_erase(t.tlo, t.thi, a.n, sh.c, &sh.hashy, bk, sh.u.m.d[tid + 1], sh.u.m.n[tid + 1],
-                                   sh.u.m.c[tid + 1], bad0 != 0);
+                                   sh.u.m.c[tid + 1], bad0 != 0, k);
   if (e & 12u) atomic_or_u32(&sh.hashy, (e & 12u) << 1);  // pre-halo / post-halo blanked: note bits 3 / 4
   if (tid == 0 && (e & 4u)) {
     sh.u.m.d[0] = sh.u.m.n[0] = sh.u.m.c[0] = 0;
@@ -1423,13 +1467,11 @@ DA_HDF uint32_t tile_p(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k, Sta
     // them opens a line (only blanks back to a newline: no comment to the
     // reference, libsvm_parser.h:91-96) -- a file header, one odd line:
     // then the walk takes their lines alone.
-    const uint64_t om = outside_mask(t, sh, tid);
-    const uint64_t wm = bk.ballot(om != 0);
-    if ((tid & (kWave - 1)) == 0 && wm) atomic_add_u32(&sh.nseg, (uint32_t)popc64(wm));
-    if (tid == 0 && sh.prebad) atomic_add_u32(&sh.nseg, 1u);
-    bk.sync();
-    if (sh.nseg <= 2u) {  // block-uniform: does every '#' of those segments open a line?
+    // (nseg: counted by commit_seg before the classify barrier; stable until the next one)
+    const uint32_t nseg = sh.nseg + (sh.prebad != 0 ? 1u : 0u);
+    if (nseg <= 2u) {  // block-uniform: does every '#' of those segments open a line?
       // (thread 0 also takes the pre-halo's bytes, first)
+      const uint64_t om = outside_mask(t, sh, tid);
       const bool pre = tid == 0 && sh.prebad && t.tlo >= (uint64_t)kPre;
       if (om || pre) {
         const uint64_t slo = t.tlo >= (uint64_t)kPre ? t.tlo - kPre : 0;
@@ -1453,7 +1495,7 @@ DA_HDF uint32_t tile_p(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k, Sta
       }
       bk.sync();
     }
-    if (sh.nseg > 2u || sh.dgate) bad = comments_reclassify(t, sh, bad, bk, k);
+    if (nseg > 2u || sh.dgate) bad = comments_reclassify(t, sh, bad, bk, k);
     FAST_STAMP(k, 12);
     bad = dirty_lines(t, sh, bad, bk, at, k);  // lines still holding bytes outside the grammar
     FAST_STAMP(k, 14);

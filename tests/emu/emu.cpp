@@ -52,6 +52,7 @@ struct BlockCtxT {
   alignas(64) unsigned char scan[NT * 64];
   uint64_t mins[NT];
   uint64_t sh8[NT];
+  uint32_t wv[NT / kWave];
   BlockCtxT() {
     for (int w = 0; w < kW; ++w) wbar.push_back(new Barrier(kWave));
   }
@@ -88,6 +89,10 @@ struct HostBlockT {
     wave_sync();
     return r;
   }
+  void wave_put(uint32_t v) {  // DevBlockT::wave_put
+    if (t % kWave == 0) ctx->wv[t / kWave] = v;
+  }
+  uint32_t wave_get(int w) { return ctx->wv[w]; }
   uint32_t wave_sum(uint32_t v) {
     ctx->ws[t] = v;
     wave_sync();

@@ -74,7 +74,9 @@ def main():
             print("  slowest classify (tile: cycles): %s" % ", ".join("%d: %d" % (k, cls[k]) for k in top))
             hz = st[:, 12] > st[:, 2]  # tiles that took the comment / dirty-line pass this run
             if hz.any():
-                for name, a0, a1 in (("comment pass", 2, 12), ("  erase", 10, 16), ("  reclassify", 16, 12),
+                for name, a0, a1 in (("comment pass", 2, 12), ("  erase", 10, 16), ("    masks+prehalo", 10, 17),
+                                     ("    scan 1", 17, 18), ("    scan 2", 18, 19), ("    blank+sync", 19, 16),
+                                     ("  reclassify", 16, 12),
                                      ("dirty: walk", 12, 13), ("dirty: rest", 13, 14)):
                     sel = hz & (st[:, a1] > 0) & (st[:, a0] > 0)
                     if not sel.any():
