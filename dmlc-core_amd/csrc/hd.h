@@ -142,6 +142,19 @@ DA_HD void spin_pause() {
 #endif
 }
 
+// Wave priority (s_setprio): a tile on the look-back chain's critical path
+// (its serial per-line walk) raised above the tiles that wait for it.
+DA_HD void prio_high() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_s_setprio(3);
+#endif
+}
+DA_HD void prio_normal() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_s_setprio(0);
+#endif
+}
+
 // v_perm_b32: byte i of the result = byte sel[i] (0..7) of {s0:s1} (s1 = bytes 0-3).
 // Callers only pass selectors 0..7.
 DA_HD uint32_t perm_b32(uint32_t s0, uint32_t s1, uint32_t sel) {

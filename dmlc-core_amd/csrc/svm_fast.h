@@ -1258,6 +1258,48 @@ DA_HDF uint32_t dirty_lines(const Tile &t, Shared &sh, uint32_t bad, BK &bk, At 
   }
   bk.sync();
   bad = reclassify_blanked(t, sh, bad, changed, parts, bk, at);
+  // the walked runs into the (blanked) planes as one-byte runs whose gaps make
+  // the role arithmetic read them as walked: a ':' before a weight or value;
+  // a label follows its line's newline or unit start (not blanked)
+  {
+    const uint32_t ne = sh.ndl;
+    const int32_t s0 = kPre + tid * kSegB;  // my segment's staged offsets; the pre-halo: thread 0's slot 0
+    uint64_t dd = 0, cc = 0, hd = 0, hc = 0;
+    for (uint32_t i = 0; i < ne; ++i) {
+      const uint32_t e = sh.dl[i];
+      const int32_t o = (int32_t)(e & 0xFFFFu);
+      const uint32_t kd = e >> 16;
+      const bool kv = kd == DK_W || kd == DK_V;
+      if (o >= s0 && o < s0 + kSegB) dd |= 1ull << (o - s0);
+      if (kv && o - 1 >= s0 && o - 1 < s0 + kSegB) cc |= 1ull << (o - 1 - s0);
+      if (tid == 0 && o < kPre) hd |= 1ull << o;
+      if (tid == 0 && kv && o - 1 >= 0 && o - 1 < kPre) hc |= 1ull << (o - 1);
+    }
+    if (dd | cc) {
+      sh.u.m.d[tid + 1] |= dd;
+      sh.u.m.c[tid + 1] |= cc;
+    }
+    if (hd | hc) {
+      sh.u.m.d[0] |= hd;
+      sh.u.m.c[0] |= hc;
+    }
+  }
+  bk.sync();
+  return bad;
+}
+
+// After the tile's aggregate is published (MODE 2, before the run lists):
+// the walked lines' bytes back into the staged text and the digit plane, for
+// the index windows.  (Done before the roles, its global round trip sat on
+// the look-back chain: every later tile waits for a dirty tile's aggregate.)
+template <class BK, class At>
+DA_HDF void dirty_restore(const Tile &t, Shared &sh, BK &bk, At at) {
+  const int tid = bk.tid();
+  const uint64_t n = t.a->n;
+  const uint32_t nr = sh.ndr;
+  const uint64_t shi = mn<uint64_t>(t.tlo + kTile + kPost, n);
+  const uint32_t parts = (sh.hashy >> 8) & 6u;
+  const uint64_t P = t.tlo + (uint64_t)tid * kSegB;
   // the lines' bytes back for the decoders (index windows: exact on any run
   // of digitchars; floats are decoded again at the end), digit-plane bits
   // from the bytes themselves (the table's G also marks bytes outside the
@@ -1305,12 +1347,14 @@ DA_HDF uint32_t dirty_lines(const Tile &t, Shared &sh, uint32_t bad, BK &bk, At 
     *dig = dg;
     return rm;
   };
-  if (changed) {
+  if (P < n) {
     uint64_t dig = 0;
     const uint64_t rm = restore(P, mn<uint64_t>(P + kSegB, n), &dig);
-    const uint64_t g = ((sh.gw[2 * tid] | ((uint64_t)sh.gw[2 * tid + 1] << 32)) & ~rm) | dig;
-    sh.gw[2 * tid] = (uint32_t)g;
-    sh.gw[2 * tid + 1] = (uint32_t)(g >> 32);
+    if (rm) {
+      const uint64_t g = ((sh.gw[2 * tid] | ((uint64_t)sh.gw[2 * tid + 1] << 32)) & ~rm) | dig;
+      sh.gw[2 * tid] = (uint32_t)g;
+      sh.gw[2 * tid + 1] = (uint32_t)(g >> 32);
+    }
   }
   if (parts & 4u) {  // the post-halo (kPost = 128 bytes): two lanes of the last wave, 64 bytes each
     if (tid >= kFThreads - 2) {
@@ -1320,34 +1364,6 @@ DA_HDF uint32_t dirty_lines(const Tile &t, Shared &sh, uint32_t bad, BK &bk, At 
       if (tid == kFThreads - 2) sh.gw[2 * kFThreads] = (uint32_t)((sh.gw[2 * kFThreads] & ~rm) | dig);
     }
   }
-  // the walked runs into the (blanked) planes as one-byte runs whose gaps make
-  // the role arithmetic read them as walked: a ':' before a weight or value;
-  // a label follows its line's newline or unit start (not blanked)
-  {
-    const uint32_t ne = sh.ndl;
-    const int32_t s0 = kPre + tid * kSegB;  // my segment's staged offsets; the pre-halo: thread 0's slot 0
-    uint64_t dd = 0, cc = 0, hd = 0, hc = 0;
-    for (uint32_t i = 0; i < ne; ++i) {
-      const uint32_t e = sh.dl[i];
-      const int32_t o = (int32_t)(e & 0xFFFFu);
-      const uint32_t kd = e >> 16;
-      const bool kv = kd == DK_W || kd == DK_V;
-      if (o >= s0 && o < s0 + kSegB) dd |= 1ull << (o - s0);
-      if (kv && o - 1 >= s0 && o - 1 < s0 + kSegB) cc |= 1ull << (o - 1 - s0);
-      if (tid == 0 && o < kPre) hd |= 1ull << o;
-      if (tid == 0 && kv && o - 1 >= 0 && o - 1 < kPre) hc |= 1ull << (o - 1);
-    }
-    if (dd | cc) {
-      sh.u.m.d[tid + 1] |= dd;
-      sh.u.m.c[tid + 1] |= cc;
-    }
-    if (hd | hc) {
-      sh.u.m.d[0] |= hd;
-      sh.u.m.c[0] |= hc;
-    }
-  }
-  bk.sync();
-  return bad;
 }
 
 // Pass 1 (libsvm): blank the comments and classify again what changed; all
@@ -1462,6 +1478,11 @@ DA_HDF uint32_t tile_p(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k, Sta
   // a byte outside the grammar ('#' among them) in the tile or in the pre-halo:
   // blank the comments and classify again (block-uniform, libsvm only)
   if (!FM && __builtin_expect(sh.hashy != 0, 0)) {
+#ifndef FSVM_NO_PRIO
+    // until its aggregate is published, this tile holds up every later
+    // tile's look-back: its waves go first (A/B: FSVM_NO_PRIO)
+    prio_high();
+#endif
     // The comment pass first, unless at most two segments (the pre-halo
     // counting as one) hold bytes outside the grammar and every '#' among
     // them opens a line (only blanks back to a newline: no comment to the
@@ -1542,6 +1563,9 @@ DA_HDF uint32_t tile_p(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k, Sta
 #if defined(FSVM_ABL_STOP) && FSVM_ABL_STOP == 2  // + roles + block scan
   if (ex == 0x123456789ull) a.res[15] = totp;
   return a.ntiles;
+#endif
+#ifndef FSVM_NO_PRIO
+  if (!FM) prio_normal();  // (every wave resets its own; one scalar instruction, no LDS read)
 #endif
   // ---- publish this tile's aggregate
   const uint32_t cnt4[4] = {nL, nI, nV, nW};  // look-back slots Q_ROWS, Q_INDEX, Q_VALUE, Q_WEIGHT
@@ -1676,6 +1700,8 @@ DA_HDF uint32_t tile_p(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k, Sta
     put_list(so.L, fb0 + nVp + fL(rel));
     put_list(so.W, fb0 + nVp + nLp + fW(rel));
   };
+  // (block-uniform: a tile whose dirty lines were walked)
+  if (MODE == 2 && !FM && sh.ndr != 0 && !sh.dgate) dirty_restore(t, sh, bk, at);
   if (MODE == 2) {
     // (the block scan's barriers ordered every plane read before these writes)
     constexpr uint32_t kIW = FM ? 2u : 1u;  // list entries per index (libfm: + its field)
