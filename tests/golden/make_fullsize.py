@@ -49,6 +49,11 @@ CONFIGS = {
     "libsvm_hdrs_1m_x128": (synth.LIBSVM_HDRS, po.LIBSVM, 1 << 20, 128, 0),
     "libsvm_1b_im1_1m_x128": (synth.LIBSVM_1B, po.LIBSVM, 1 << 20, 128, 0),
     "libfm_1m_x64": (synth.LIBFM, po.LIBFM, 1 << 20, 64, 0),
+    # round 5: the CSV label / weight-column single pass (csv_fast_tile_sp)
+    # and libfm's exact kernels at full size
+    "csv_label0_1m_x256": (synth.CSV, po.CSV, 1 << 20, 256, 0),
+    "csv_lw_1m_x256": (synth.CSV, po.CSV, 1 << 20, 256, 0),
+    "libfm_exact_1m_x64": (synth.LIBFM, po.LIBFM, 1 << 20, 64, 0),
 }
 for _r in range(8):  # config 5: bench.py's rank r shard of 32M x 64 (4M rows from row r * 4M)
     CONFIGS["libsvm_32m_x64_part%d" % _r] = (synth.LIBSVM, po.LIBSVM, 4 << 20, 64, _r * (4 << 20))
@@ -58,8 +63,10 @@ for _r in range(8):  # config 5: bench.py's rank r shard of 32M x 64 (4M rows fr
 PARAMS = {
     "libsvm_nt2_1m_x128": {"nthread": 2},
     "libsvm_1b_im1_1m_x128": {"indexing_mode": -1},
+    "csv_label0_1m_x256": {"label_column": 0},
+    "csv_lw_1m_x256": {"label_column": 3, "weight_column": 7},
 }
-FLAGS = {"libsvm_exact_1m_x128": ("exact", 1), "csv_exact_1m_x256": ("exact", 1)}
+FLAGS = {"libsvm_exact_1m_x128": ("exact", 1), "csv_exact_1m_x256": ("exact", 1), "libfm_exact_1m_x64": ("exact", 1)}
 
 
 def stream_chunks(sfmt, rows, width, row0, block_rows):
