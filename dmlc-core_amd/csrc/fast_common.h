@@ -803,7 +803,18 @@ DA_HDF void stage_issue(const uint8_t *text, uint64_t n, uint64_t tlo, StageRegs
 #pragma unroll
   for (int i = 0; i < kStageRounds; ++i) {
     const int u = t + i * kFThreads;
+#if defined(FSVM_NT_STAGE) && defined(__HIP_DEVICE_COMPILE__)  // A/B: streaming (non-temporal) text loads
+    if (u < kStageUnits) {
+      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+      const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(src + 16 * u));
+      r.w[i][0] = v.x;
+      r.w[i][1] = v.y;
+      r.w[i][2] = v.z;
+      r.w[i][3] = v.w;
+    }
+#else
     if (u < kStageUnits) load16(src + 16 * u, r.w[i]);
+#endif
   }
 }
 template <class BK>

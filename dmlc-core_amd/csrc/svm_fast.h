@@ -988,6 +988,16 @@ DA_HDF uint32_t classify_tile(const Tile &t, Shared &sh, int tid, At at, bool fi
   return bad;
 }
 
+// CSR stores (A/B FSVM_NT_STORE: non-temporal -- the outputs are written once)
+template <class T>
+DA_HD void out_store(T *p, T v) {
+#if defined(FSVM_NT_STORE) && defined(__HIP_DEVICE_COMPILE__)
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
+
 // ---- per-line fallback.  A line holding bytes outside the grammar (after
 // the tile's comments are blanked) -- a "# header" line of the next file that
 // InputSplit put mid-chunk (input_split_base.cc:204-210), which the reference
@@ -1744,8 +1754,14 @@ DA_HDF uint32_t tile_p(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k, Sta
 #else
   if (tid < kWave) {
 #endif
+#ifdef FSVM_LB_PRIO  // A/B: the look-back wave ahead of the other tiles' waves
+    prio_high();
+#endif
     const uint32_t rounds =
         look_back(a.lb, a.ntiles, k, cnt4, a.gate, sh.c, bk);
+#ifdef FSVM_LB_PRIO
+    prio_normal();
+#endif
 #if defined(DMLC_AMD_STAMPS) && defined(__HIP_DEVICE_COMPILE__)
     if (tid == 0 && k < kStampTiles) g_stamps[(uint64_t)k * kStampSlots + 15] = rounds;
 #else
@@ -1820,8 +1836,8 @@ DA_HDF uint32_t tile_p(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k, Sta
       return;
     }
     if (r < a.cap[C_INDEX]) {
-      if (a.wide) reinterpret_cast<uint64_t *>(a.index)[r] = v;
-      else reinterpret_cast<uint32_t *>(a.index)[r] = (uint32_t)v;
+      if (a.wide) out_store(reinterpret_cast<uint64_t *>(a.index) + r, v);
+      else out_store(reinterpret_cast<uint32_t *>(a.index) + r, (uint32_t)v);
     } else {
       raise_error(a.err, E_CAPACITY, q);
     }
@@ -1831,11 +1847,11 @@ DA_HDF uint32_t tile_p(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k, Sta
     if (v == 1234.5f) a.res[15] = r;
     return;
 #endif
-    if (r < a.cap[C_VALUE]) a.value[r] = v;
+    if (r < a.cap[C_VALUE]) out_store(a.value + r, v);
     else raise_error(a.err, E_CAPACITY, q);
   };
   auto put_label = [&](uint64_t r, float v, uint64_t q) {
-    if (r < a.cap[C_ROWS]) a.label[r] = v;
+    if (r < a.cap[C_ROWS]) out_store(a.label + r, v);
     else raise_error(a.err, E_CAPACITY, q);
   };
   auto put_weight = [&](uint64_t r, float v, uint64_t q) {
@@ -1885,7 +1901,7 @@ DA_HDF uint32_t tile_p(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k, Sta
   uint64_t rl = eL;
   for (uint64_t m = so.L; m; m &= m - 1, ++rl) {
     const uint64_t below = (m & (0 - m)) - 1;
-    if (inb || rl < a.cap[C_ROWS]) a.offset[rl] = eI + popc64(so.I & below);
+    if (inb || rl < a.cap[C_ROWS]) out_store(a.offset + rl, (uint64_t)(eI + popc64(so.I & below)));
     else raise_error(a.err, E_CAPACITY, P + ctz64(m));
   }
   if constexpr (!FM) {
