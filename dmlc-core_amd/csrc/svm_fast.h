@@ -158,6 +158,7 @@ struct Shared {  // LDS of one workgroup
   uint32_t gw[2 * kFThreads + 2];  // digit plane as words: 2t, 2t+1 segment t; 2 kFThreads: the post-halo
   uint64_t pend[kPendWords];  // packed inclusive counts at the end of each pass (dirty_lines: wave masks)
   uint64_t prebad;            // pre-halo bytes outside the grammar (dirty_lines)
+  uint64_t qfail[kFWaves];    // segments whose first-pass "qid:" check failed (the comment pass's plane path)
   uint32_t npass;
   uint32_t next;   // persistent form: the next tile id
   uint32_t nq;     // qid runs of the tile
@@ -469,7 +470,8 @@ DA_HD uint64_t cs_bits(const TileCommon &c, uint64_t lo) {
 // every wave through the slowest lane's segment.
 template <class BK>
 DA_HDF uint32_t comment_erase(uint64_t tlo, uint64_t thi, uint64_t n, TileCommon &c, uint32_t *note, BK &bk,
-                              uint64_t D, uint64_t N, uint64_t C, bool raw, uint32_t k) {
+                              uint64_t D, uint64_t N, uint64_t C, bool raw, uint32_t k, bool planes_ok,
+                              uint64_t *Mplanes) {
   (void)k;  // (phase stamps of the diagnostic build)
   const int tid = bk.tid();
   const uint32_t lane = (uint32_t)tid & (kWave - 1), wbase = (uint32_t)tid - lane;
@@ -556,11 +558,24 @@ DA_HDF uint32_t comment_erase(uint64_t tlo, uint64_t thi, uint64_t n, TileCommon
   FAST_STAMP(k, 19);
   uint32_t co, gate = 0;
   const uint64_t M = comment_mask(A, B, cin, &co);
+  // Every comment is blanked in the staged text (the per-line walk and the
+  // decoders read it).  A segment whose first-pass "qid:" checks all held
+  // (planes_ok) then takes its comment out of its planes (*Mplanes; the
+  // caller clears the bits) instead of being classified again: its planes
+  // are exactly the reclassified ones (the comment bytes read as blanks,
+  // the rest as classified -- a qid token next to a comment fails the check)
+#ifndef FSVM_CMT_BLANK  // A/B: every comment blanked and reclassified
+  const bool via_planes = M != 0 && planes_ok;
+#else
+  const bool via_planes = false;
+  (void)planes_ok;
+#endif
+  *Mplanes = via_planes ? M : 0;
   for (uint64_t m = bk.ballot(M != 0); m; m &= m - 1) {  // wave-uniform
     const uint32_t s = (uint32_t)ctz64(m);
     wave_blank(txt + kPre + (wbase + s) * kSegB, M, s, bk);
   }
-  uint32_t changed = M != 0;  // bit 0: my segment, bit 1: the pre-halo, bit 2: the post-halo
+  uint32_t changed = M != 0 && !via_planes;  // bit 0: my segment, bit 1: the pre-halo, bit 2: the post-halo
   if (tid < kWave && tlo > 0) {  // wave 0: lane 0's pre-halo comment bytes
     uint32_t ch;
     const uint64_t Mh = comment_mask(hA, hB, 0u, &ch);
@@ -937,7 +952,10 @@ DA_HDF uint32_t commit_seg(const Tile &t, Shared &sh, int seg, At at, bool first
   const uint64_t P0 = t.tlo + (uint64_t)seg * kSegB;
   if ((m.n & m.c) || ((m.c & 1) && P0 > 0 && is_qid_letter(at(P0 - 1)))) {  // letters: "qid:" tokens
     auto wd = [&](uint64_t p) -> uint32_t { return text_word(t, p, at); };
-    if (FM || !qid_clean(P0, &m.n, &m.c, P0 > 0 && is_qid_letter(at(P0 - 1)), at, wd)) bad = 1;
+    if (FM || !qid_clean(P0, &m.n, &m.c, P0 > 0 && is_qid_letter(at(P0 - 1)), at, wd)) {
+      bad = 1;
+      if (!FM && first) atomic_or_u64(&sh.qfail[seg / kWave], 1ull << (seg % kWave));
+    }
   }
   sh.gw[2 * seg] = (uint32_t)m.g;
   sh.gw[2 * seg + 1] = (uint32_t)(m.g >> 32);
@@ -1385,8 +1403,20 @@ DA_HDF uint32_t comments_reclassify(const Tile t, Shared &sh, uint32_t bad0, BK 
   (void)k;  // (phase stamps of the diagnostic build)
   const int tid = bk.tid();
   const FastSvmArgs &a = *t.a;
+  uint64_t Mp = 0;
+  const bool planes_ok = !((sh.qfail[tid / kWave] >> (tid % kWave)) & 1u);
   const uint32_t e = comment_erase(t.tlo, t.thi, a.n, sh.c, &sh.hashy, bk, sh.u.m.d[tid + 1], sh.u.m.n[tid + 1],
-                                   sh.u.m.c[tid + 1], bad0 != 0, k);
+                                   sh.u.m.c[tid + 1], bad0 != 0, k, planes_ok, &Mp);
+  if (Mp) {  // my segment's comment out of its planes; its flag: bytes outside the grammar left
+    const uint64_t d = sh.u.m.d[tid + 1] & ~Mp;
+    sh.u.m.d[tid + 1] = d;
+    sh.u.m.n[tid + 1] &= ~Mp;
+    sh.u.m.c[tid + 1] &= ~Mp;
+    const uint64_t g = (sh.gw[2 * tid] | ((uint64_t)sh.gw[2 * tid + 1] << 32)) & ~Mp;
+    sh.gw[2 * tid] = (uint32_t)g;
+    sh.gw[2 * tid + 1] = (uint32_t)(g >> 32);
+    bad0 = (g & ~d) != 0 ? 1u : 0u;
+  }
   if (e & 12u) atomic_or_u32(&sh.hashy, (e & 12u) << 1);  // pre-halo / post-halo blanked: note bits 3 / 4
   if (tid == 0 && (e & 4u)) {
     sh.u.m.d[0] = sh.u.m.n[0] = sh.u.m.c[0] = 0;
@@ -1460,6 +1490,7 @@ DA_HDF uint32_t tile_p(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k, Sta
   if (tid == 0) {
     sh.u.m.d[0] = sh.u.m.n[0] = sh.u.m.c[0] = 0;
     sh.nq = 0;
+    for (int w = 0; w < kFWaves; ++w) sh.qfail[w] = 0;
     sh.hashy = 0;
     sh.prebad = 0;
     sh.ndl = sh.ndr = sh.nseg = sh.dgate = 0;
