@@ -100,6 +100,12 @@ struct FastSvmArgs {
   unsigned long long *err;  // first error of this path
   uint64_t *res;        // dmlc_amd_result counts (written by the last tile)
   uint32_t *ticket;     // persistent launch: tiles handed out past the first gridDim.x (zeroed per launch)
+  // the lean kernel (svm_lean.h) ahead of this one: its look-back words [5 ntiles]
+  // and ~(its first poisoned tile) (0: none), zeroed per launch.  The full
+  // kernel resumes at that tile, its look-back seeded by the lean inclusive
+  // prefix before it (null: no lean launch, the full kernel takes every tile).
+  uint64_t *lean_lb;
+  uint64_t *lean_poison;
 };
 
 // look-back words per single-pass tile (fast_common.h: status + 4 prefix words);

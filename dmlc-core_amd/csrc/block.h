@@ -128,6 +128,33 @@ struct DevBlockT {
     return pre + inc - v;
   }
 
+  // Exclusive prefix sum of packed counters (fields never carry across bit
+  // 31) with one barrier, and the OR of a flag over the block: each wave's
+  // total and flag go to wtot / wbad (caller's LDS, never rewritten before
+  // the workgroup ends), every thread then reads all of them.
+  // *wpre: the exclusive prefix at the wave's first lane.
+  __device__ __forceinline__ uint64_t exclusive_add1(uint64_t v, bool flag, uint64_t *wtot, uint32_t *wbad,
+                                                     uint64_t *total, uint64_t *wpre) const {
+    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+    const uint64_t inc = wave_incl_add((uint32_t)v) | ((uint64_t)wave_incl_add((uint32_t)(v >> 32)) << 32);
+    const uint64_t fm = __ballot(flag);
+    if (lane == kWave - 1) {
+      wtot[wid] = inc;
+      wbad[wid] = fm != 0 ? 1u : 0u;
+    }
+    __syncthreads();
+    uint64_t pre = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      const uint64_t t = wtot[w];
+      pre += w < wid ? t : 0;
+      tot += t;
+    }
+    *total = tot;
+    *wpre = pre;
+    return pre + inc - v;
+  }
+
   // The same with one barrier: every wave reads all wave totals itself.  The
   // scratch slots stay read until the caller's next barrier, so a second
   // scan must not follow before one.

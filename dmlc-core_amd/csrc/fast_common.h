@@ -868,10 +868,14 @@ constexpr uint64_t kMark = 1ull << 63;
 #ifndef FSVM_LB_DRAIN
 
 // Lane 0: publish this tile's aggregate (tile 0 publishes its inclusive).
-DA_HD void publish_aggregate(uint64_t *lb, uint32_t ntiles, uint32_t k, const uint32_t cnt[4]) {
+// kf / seed: a launch that resumes at tile kf (svm_lean.h) -- tile kf is the
+// first, its exclusive prefix is seed[4] (tagged inclusive words of the
+// launch before: the mark is dropped).
+DA_HD void publish_aggregate(uint64_t *lb, uint32_t ntiles, uint32_t k, const uint32_t cnt[4], uint32_t kf = 0,
+                             const uint64_t *seed = nullptr) {
   uint64_t *st = lb, *incl = lb + ntiles;
-  if (k == 0) {
-    for (int i = 0; i < 4; ++i) store_agent_u64(incl + i, kMark | cnt[i]);
+  if (k == kf) {
+    for (int i = 0; i < 4; ++i) store_agent_u64(incl + (uint64_t)k * 4 + i, kMark | ((seed ? seed[i] & ~kMark : 0) + cnt[i]));
   } else {
     store_agent_u64(st + k, kSAgg | pack4(cnt));
   }
@@ -886,13 +890,15 @@ DA_HD void publish_aggregate(uint64_t *lb, uint32_t ntiles, uint32_t k, const ui
 // synchronises.
 template <class BK>
 DA_HDF uint32_t look_back(uint64_t *lb, uint32_t ntiles, uint32_t k, const uint32_t cnt[4], uint32_t *gate,
-                          TileCommon &c, BK &bk) {
+                          TileCommon &c, BK &bk, uint32_t kf = 0, const uint64_t *seed = nullptr) {
   const uint32_t lane = bk.tid();
   uint64_t *st = lb, *incl = lb + ntiles;
   uint64_t j = k;
   uint32_t spins = 0, rounds = 0;
   uint64_t acc[4] = {0, 0, 0, 0};
-  bool done = k == 0;
+  if (k == kf && seed)
+    for (int f = 0; f < 4; ++f) acc[f] = seed[f] & ~kMark;
+  bool done = k == kf;  // (a resumed launch: tile kf published its inclusive prefix, svm_lean.h)
   while (!done) {
     ++rounds;
     uint64_t s = 0, w[4] = {kMark, kMark, kMark, kMark};  // before tile 0: an inclusive 0
@@ -935,7 +941,7 @@ DA_HDF uint32_t look_back(uint64_t *lb, uint32_t ntiles, uint32_t k, const uint3
   if (lane < 4) {
     const uint64_t v = acc[lane == 0 ? 0 : lane == 1 ? 1 : lane == 2 ? 2 : 3];
     c.base[lane] = v;
-    if (k > 0) store_agent_u64(incl + (uint64_t)k * 4 + lane, kMark | (v + cnt[lane == 0 ? 0 : lane == 1 ? 1 : lane == 2 ? 2 : 3]));
+    if (k > kf) store_agent_u64(incl + (uint64_t)k * 4 + lane, kMark | (v + cnt[lane == 0 ? 0 : lane == 1 ? 1 : lane == 2 ? 2 : 3]));
   }
   return rounds;
 }

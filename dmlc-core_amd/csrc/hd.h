@@ -61,6 +61,16 @@ DA_HD void atomic_min_u64(unsigned long long *p, unsigned long long v) {
 #endif
 }
 
+DA_HD void atomic_max_u64(unsigned long long *p, unsigned long long v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  atomicMax(p, v);
+#else
+  unsigned long long cur = __atomic_load_n(p, __ATOMIC_RELAXED);
+  while (v > cur && !__atomic_compare_exchange_n(p, &cur, v, true, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) {
+  }
+#endif
+}
+
 // atomic min, skipped when a plain read already shows a value <= v: minima
 // of many tiles on one word (a ParseBlock unit's) mostly do not improve it,
 // and same-address device atomics serialise (a stale read only costs an

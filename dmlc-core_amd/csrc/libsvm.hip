@@ -12,6 +12,7 @@
 #include "libsvm_core.h"
 #include "scan.h"
 #include "svm_fast.h"
+#include "svm_lean.h"
 
 namespace dmlc_amd {
 namespace {
@@ -79,6 +80,30 @@ __global__ void __launch_bounds__(fast::kFThreads, FSVM_MINW) svm_fast_tile(Fast
 #else
   fsvm::tile<MODE>(a, sh, bk, blockIdx.x);
 #endif
+}
+
+// The lean single-pass kernel (svm_lean.h), ahead of svm_fast_tile<2> in a
+// full call: budgeted for 8 workgroups per CU (64 VGPRs).
+#ifndef LSVM_MINW
+#define LSVM_MINW 6
+#endif
+static_assert(sizeof(lsvm::Shared) <= 160 * 1024 / LSVM_MINW, "svm_lean_tile LDS above its occupancy budget");
+__global__ void __launch_bounds__(fast::kFThreads, LSVM_MINW) svm_lean_tile(FastSvmArgs a) {
+  __shared__ __attribute__((aligned(16))) lsvm::Shared sh;
+  DevBlockS bk{nullptr};
+  lsvm::tile(a, sh, bk, blockIdx.x);
+}
+// DMLC_AMD_LEAN=0 / 1 turns the lean kernel off / on (A/B timing; off, the
+// full kernel takes every tile, as before round 6); LSVM_DEFAULT the default
+#ifndef LSVM_DEFAULT
+#define LSVM_DEFAULT 0
+#endif
+bool lean_enabled() {
+  static const int on = [] {
+    const char *e = getenv("DMLC_AMD_LEAN");
+    return e && e[0] ? (e[0] == '0' ? 0 : 1) : LSVM_DEFAULT;
+  }();
+  return on != 0;
 }
 
 // workgroups of a persistent single-pass launch: what the device holds at
@@ -155,6 +180,10 @@ hipError_t launch_libsvm(const LibsvmArgs &a, const FastSvmArgs &f, bool use_fas
   }
   if (phase != kPhaseCount) fl.add(f.chunk_tab, (uint64_t)f.nchunk * 8, ~0ull);
   fl.add(reinterpret_cast<uint64_t *>(f.err), 1, ~0ull);
+  // the lean kernel first on a full call (indexing_mode < 0 and the count /
+  // fill phases stay on svm_fast_tile alone)
+  const bool lean = use_fast && phase == kPhaseFull && f.indexing_mode >= 0 && f.lean_lb && lean_enabled();
+  if (lean) fl.add(f.lean_lb, (uint64_t)f.ntiles * fast::kLbWords + 1, 0);  // + the poison word
   if (use_fast) {
     fl.add(f.lb, (uint64_t)f.ntiles * fast::kLbWords + 1, 0);  // + the ticket word
     fl.add(f.qsum, kLabShards * 8, 0);
@@ -163,14 +192,23 @@ hipError_t launch_libsvm(const LibsvmArgs &a, const FastSvmArgs &f, bool use_fas
   if (phase != kPhaseFill && a.indexing_mode < 0) fl.add(a.chunk_min, (uint64_t)a.nchunk, ~0ull);
   if (!a.ntiles && phase != kPhaseCount) fl.add(a.offset, 1, 0);  // empty input: offset = {0}
   if ((e = launch_prologue(fl, s)) != hipSuccess) return e;
+  FastSvmArgs fa = f;  // the full kernel on its own (no lean launch ahead of it)
+  fa.lean_lb = fa.lean_poison = nullptr;
   if (use_fast) {
     if (phase == kPhaseCount) {
       prof_mark(0, s, "svm_fast_tile<1>");
-      svm_fast_tile<1><<<FSVM_PERSIST ? persistent_grid(svm_fast_tile<1>, f.ntiles) : f.ntiles, fast::kFThreads, 0, s>>>(f);
+      svm_fast_tile<1><<<FSVM_PERSIST ? persistent_grid(svm_fast_tile<1>, f.ntiles) : f.ntiles, fast::kFThreads, 0, s>>>(fa);
       prof_mark(1, s, "svm_fast_tile<1>");
+    } else if (lean) {
+      // the full kernel resumes at the first tile the lean one poisoned (all
+      // of its workgroups exit at once when none did)
+      prof_mark(0, s, "svm_lean_tile");
+      svm_lean_tile<<<f.ntiles, fast::kFThreads, 0, s>>>(f);
+      prof_mark(1, s, "svm_lean_tile");
+      svm_fast_tile<2><<<f.ntiles, fast::kFThreads, 0, s>>>(f);
     } else {
       prof_mark(0, s, "svm_fast_tile<2>");
-      svm_fast_tile<2><<<FSVM_PERSIST ? persistent_grid(svm_fast_tile<2>, f.ntiles) : f.ntiles, fast::kFThreads, 0, s>>>(f);
+      svm_fast_tile<2><<<FSVM_PERSIST ? persistent_grid(svm_fast_tile<2>, f.ntiles) : f.ntiles, fast::kFThreads, 0, s>>>(fa);
       prof_mark(1, s, "svm_fast_tile<2>");
     }
     // the qid decision (qid_fix_kernel) is folded into the exact count

@@ -93,7 +93,10 @@ __global__ void recount_flag_kernel(uint32_t *gate) { gate[2] = (gate[0] != 0 &&
 // the stream costs a few microseconds: the set-up used to be six memsets and
 // the finish two kernels).  Prologue: fill up to kFillRegions word ranges and
 // set the gate word.
-constexpr int kFillRegions = 10;
+// (launch_libsvm's largest list is 10: indexing_mode < 0 on empty input.)
+// A region past kFillRegions is never dropped silently: add() notes the
+// overflow and launch_prologue refuses the call.
+constexpr int kFillRegions = 12;
 struct FillList {
   uint64_t *p[kFillRegions];
   uint64_t n[kFillRegions];
@@ -101,13 +104,17 @@ struct FillList {
   uint32_t *gate;  // set to gate_v when non-null
   uint32_t gate_v;
   int count;
+  int overflow;
   DA_HD void add(uint64_t *ptr, uint64_t words, uint64_t value) {
-    if (ptr && words && count < kFillRegions) {
-      p[count] = ptr;
-      n[count] = words;
-      v[count] = value;
-      ++count;
+    if (!ptr || !words) return;
+    if (count >= kFillRegions) {
+      overflow = 1;
+      return;
     }
+    p[count] = ptr;
+    n[count] = words;
+    v[count] = value;
+    ++count;
   }
 };
 __global__ void __launch_bounds__(256) prologue_kernel(FillList f) {
@@ -117,6 +124,7 @@ __global__ void __launch_bounds__(256) prologue_kernel(FillList f) {
     for (uint64_t i = t; i < f.n[r]; i += stride) f.p[r][i] = f.v[r];
 }
 inline hipError_t launch_prologue(const FillList &f, hipStream_t s) {
+  if (f.overflow) return hipErrorInvalidValue;  // a buffer would stay unset
   uint64_t most = 1;
   for (int r = 0; r < f.count; ++r) most = f.n[r] > most ? f.n[r] : most;
   uint64_t blocks = (most + 1023) / 1024;  // four words per thread on the largest range

@@ -1463,6 +1463,17 @@ DA_HDF uint32_t tile_p(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k, Sta
   // publish, kSpinLimit bounds the wait and the exact kernels take over.
   const int tid = bk.tid();
   if (!PERSIST && a.skip_if_gated && *a.gate) return a.ntiles;  // fill phase after an exact-path count: block-uniform
+  // after the lean kernel (svm_lean.h): resume at its first poisoned tile kf
+  // (the word holds ~kf; 0: none poisoned, nothing left to do), tile kf's
+  // exclusive prefix seeded by the lean inclusive prefix of tile kf - 1
+  uint32_t kf = 0;
+  const uint64_t *seed = nullptr;  // tile kf's exclusive prefix: the lean inclusive words of kf - 1 (marked)
+  if (!PERSIST && a.lean_poison) {
+    const uint64_t pw = *a.lean_poison;  // stable: the lean launch has finished
+    kf = pw ? (uint32_t)mn<uint64_t>(~pw, (uint64_t)a.ntiles) : a.ntiles;
+    if (k < kf) return a.ntiles;  // block-uniform
+    if (k == kf && kf > 0) seed = a.lean_lb + (uint64_t)a.ntiles + (uint64_t)(kf - 1) * 4;
+  }
   FAST_STAMP(k, 0);
   FAST_STAMP(k, 1);
   Tile t;
@@ -1611,7 +1622,7 @@ DA_HDF uint32_t tile_p(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k, Sta
   // ---- publish this tile's aggregate
   const uint32_t cnt4[4] = {nL, nI, nV, nW};  // look-back slots Q_ROWS, Q_INDEX, Q_VALUE, Q_WEIGHT
   if (tid == 0) {
-    publish_aggregate(a.lb, a.ntiles, k, cnt4);
+    publish_aggregate(a.lb, a.ntiles, k, cnt4, kf, seed);
     if (sh.c.bad) atomic_or_u32(a.gate, 1u);
     if (!FM && sh.nq) {  // the qid decision's sum (libsvm.hip), and the "some qid" word
       atomic_add_u64(a.qsum + (k % kLabShards) * 8, sh.nq);
@@ -1789,7 +1800,7 @@ DA_HDF uint32_t tile_p(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k, Sta
     prio_high();
 #endif
     const uint32_t rounds =
-        look_back(a.lb, a.ntiles, k, cnt4, a.gate, sh.c, bk);
+        look_back(a.lb, a.ntiles, k, cnt4, a.gate, sh.c, bk, kf, seed);
 #ifdef FSVM_LB_PRIO
     prio_normal();
 #endif

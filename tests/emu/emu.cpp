@@ -18,6 +18,7 @@
 #include "libfm_core.h"
 #include "libsvm_core.h"
 #include "svm_fast.h"
+#include "svm_lean.h"
 
 using namespace dmlc_amd;
 
@@ -109,6 +110,32 @@ struct HostBlockT {
     for (int i = 0; i < NT; ++i) r = ctx->mins[i] < r ? ctx->mins[i] : r;
     sync();
     return r;
+  }
+  template <typename T>
+  T shfl_up(T v, int d) {  // lane - d's value (own below d)
+    static_assert(sizeof(T) <= 8, "shfl element");
+    std::memcpy(&ctx->sh8[t], &v, sizeof(T));
+    wave_sync();
+    T r = v;
+    if (t % kWave >= d) std::memcpy(&r, &ctx->sh8[t - d], sizeof(T));
+    wave_sync();
+    return r;
+  }
+  // DevBlockT::exclusive_add1: packed counters, per-wave totals / flags to the caller's LDS
+  uint64_t exclusive_add1(uint64_t v, bool flag, uint64_t *wtot, uint32_t *wbad, uint64_t *total, uint64_t *wpre) {
+    const uint64_t fm = ballot(flag);
+    struct Add {
+      uint64_t operator()(uint64_t a, uint64_t b) const { return a + b; }
+    };
+    const uint64_t ex = exclusive(v, (uint64_t)0, Add(), total);
+    const uint64_t w0 = shfl(ex, 0);  // the wave's first lane
+    if (t % kWave == kWave - 1) {
+      wtot[t / kWave] = ex + v - w0;  // the wave's total
+      wbad[t / kWave] = fm != 0 ? 1u : 0u;
+    }
+    *wpre = w0;
+    sync();
+    return ex;
   }
   uint64_t exclusive_add(uint64_t v, uint64_t *total) {  // DevBlock::exclusive_add (packed counters)
     struct Add {
@@ -288,6 +315,22 @@ extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *c
       f.gate = &gate;
       f.err = &ferr;
       f.res = res;
+      // the lean kernel first on a full call (libsvm.hip launch_libsvm)
+      const char *le = std::getenv("DMLC_AMD_LEAN");
+      const bool lean = !fm && !count_only && prm->indexing_mode >= 0 && !(le && le[0] == '0');  // (on unless turned off)
+      std::vector<uint64_t> llb(nft * 5 + 1, 0);
+      if (lean) {
+        f.lean_lb = llb.data();
+        f.lean_poison = llb.data() + nft * 5;
+        for (uint64_t k = 0; k < nft; ++k) {
+          lsvm::Shared *sh = new lsvm::Shared;
+          std::memset(sh, 0xCD, sizeof(*sh));
+          run_block<fast::kFThreads>([&](FastBlock &bk) { lsvm::tile(f, *sh, bk, (uint32_t)k); });
+          delete sh;
+        }
+        if (std::getenv("EMU_VERBOSE"))
+          std::fprintf(stderr, "emu: lean poison=%lld\n", llb[nft * 5] ? (long long)~llb[nft * 5] : -1ll);
+      }
       for (uint64_t k = 0; k < nft; ++k) {
         fsvm::Shared *sh = new fsvm::Shared;
         std::memset(sh, 0xCD, sizeof(*sh));

@@ -3,6 +3,8 @@
 The emulator executes the same per-thread code as the HIP kernels
 (dmlc-core_amd/csrc/*_core.h) with 256 host threads per workgroup; these tests
 catch logic and memory-safety bugs in the kernel bodies without a GPU."""
+import os
+
 import numpy as np
 import pytest
 
@@ -295,10 +297,19 @@ def test_emu_fast_many_chunks():
             offs = _many_chunks(rng, data, n_cuts, cluster)
             f = po.LIBSVM if fmt == "libsvm" else po.CSV
             o = po.parse_chunks(data, offs, fmt=f)
-            h = pyemu.parse(data, offs, fmt)
-            assert o["status"] == 0 and not check_fail(h, fmt, offs)
-            assert diff(h, o) == [], (fmt, n_cuts, diff(h, o))
-            assert h["path"] == ("exact" if cluster else "fast"), (fmt, n_cuts, h["path"])
+            # libsvm: the lean kernel (svm_lean.h) takes up to 63 unit starts
+            # per wave, so the cluster stays on the single pass; the full
+            # kernel alone (DMLC_AMD_LEAN=0) hands it to the exact kernels
+            for lean in (("1", "0") if fmt == "libsvm" else ("1",)):
+                os.environ["DMLC_AMD_LEAN"] = lean
+                try:
+                    h = pyemu.parse(data, offs, fmt)
+                finally:
+                    os.environ.pop("DMLC_AMD_LEAN", None)
+                assert o["status"] == 0 and not check_fail(h, fmt, offs)
+                assert diff(h, o) == [], (fmt, n_cuts, lean, diff(h, o))
+                want = "exact" if cluster and (fmt == "csv" or lean == "0") else "fast"
+                assert h["path"] == want, (fmt, n_cuts, lean, h["path"])
 
 
 def test_emu_csv_fast_label_column():
