@@ -146,12 +146,18 @@ uint64_t rec_bytes_of(uint64_t nbytes, uint64_t T, uint64_t ntiles, const dmlc_a
   return dmlc_amd::exact_rec_on(nbytes, b) ? b : 0;
 }
 
+// single-pass look-back words: the full kernel's [5 nft] + its ticket; libsvm
+// adds the lean kernel's [5 nft] + its poison word (libsvm.hip)
+uint64_t lb_words_of(uint64_t nft, const dmlc_amd_params *prm) {
+  return prm && prm->format == DMLC_AMD_LIBSVM ? nft * 10 + 2 : nft * 5 + 1;
+}
+
 size_t dmlc_amd_workspace_bytes(uint64_t nbytes, int nchunks, const dmlc_amd_params *prm) {
   const uint64_t T = tile_of(prm);
   const uint64_t ntiles = (nbytes + T - 1) / T;
   const uint64_t nc = (nchunks > 0 ? (uint64_t)nchunks : 1) * (uint64_t)units_per_chunk(prm);
   const uint64_t nft = (nbytes + kFastTile - 1) / kFastTile;
-  return (size_t)((2 * ntiles * kSlots + 2 * nc + nc * 8 + (nc + 1) + nft * 10 + 2 + dmlc_amd::kLabShards * 8) *
+  return (size_t)((2 * ntiles * kSlots + 2 * nc + nc * 8 + (nc + 1) + lb_words_of(nft, prm) + dmlc_amd::kLabShards * 8) *
                       sizeof(uint64_t) +
                   12 * 256 + rec_bytes_of(nbytes, T, ntiles, prm) + 2 * 256);
 }
@@ -189,9 +195,7 @@ int dmlc_amd_parse(const void *d_text, uint64_t nbytes, const uint64_t *d_chunk_
   const uint64_t nft = (nbytes + kFastTile - 1) / kFastTile;
   uint32_t *ctl = cv.take<uint32_t>(4);               // gate, gate after the count phase, recount flag
   unsigned long long *ferr = cv.take<unsigned long long>(1);
-  // single-pass look-back words: the full kernel's [5 nft] + its ticket, then
-  // the lean kernel's [5 nft] + its poison word (libsvm.hip)
-  uint64_t *lb = cv.take<uint64_t>(nft * 10 + 2);
+  uint64_t *lb = cv.take<uint64_t>(lb_words_of(nft, prm));
   uint64_t *labsum = cv.take<uint64_t>(dmlc_amd::kLabShards * 8);
   const uint64_t recb = rec_bytes_of(nbytes, T, ntiles, prm);
   const uint32_t rec_win = dmlc_amd::exact_rec_win(T, dmlc_amd::kWin);

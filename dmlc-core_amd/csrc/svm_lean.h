@@ -349,6 +349,8 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
   const uint64_t thi = mn<uint64_t>(tlo + kTile, n);
   const uint64_t P = tlo + (uint64_t)tid * kSegB;
   const uint64_t P0 = tlo + (uint64_t)wid * kWave * kSegB;  // the wave's first segment
+  FAST_STAMP(k, 0);
+  FAST_STAMP(k, 1);
   // ---- loads: my 64 bytes, the 64 bytes before my wave (lane = byte), the
   // post-halo (the last wave's lanes 60-63)
   // (a segment or post-halo piece reaching past the text end -- the last
@@ -394,6 +396,7 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
   // scalar and vector L1s, which another CU's atomic does not update)
   if (tid == 0) sh.flags = ~load_agent_u64(a.lean_poison) < (uint64_t)k ? 1u : 0u;
   bk.sync();
+  FAST_STAMP(k, 2);
   if (sh.flags & 1u) {  // a tile before this one poisoned: the full kernel takes it from there
     if (tid == 0) store_agent_u64(a.lean_lb + k, kSPoison);  // (a look-back of a later tile must not wait for this one)
     return;
@@ -464,6 +467,7 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
   ro.bad = 0;
   if (P < n) ro = lean_roles(m.d & valid, m.n & valid, m.c & valid, S, valid, at_end, dc, ginl, ginc, prole);
   bad |= ro.bad;
+  FAST_STAMP(k, 3);
   // ---- block scan of the packed role counts (one barrier), poison flag with it
   const uint64_t mine = (uint64_t)popc64(ro.L) | ((uint64_t)popc64(ro.W) << 16) | ((uint64_t)popc64(ro.I) << 32) |
                         ((uint64_t)popc64(ro.V) << 48);
@@ -483,6 +487,7 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
   }
   const uint32_t cnt4[4] = {nL, nI, nV, nW};  // look-back slots fsvm Q_ROWS, Q_INDEX, Q_VALUE, Q_WEIGHT
   if (tid == 0) publish_aggregate(a.lean_lb, a.ntiles, k, cnt4);
+  FAST_STAMP(k, 4);
 #if defined(LSVM_ABL) && LSVM_ABL == 1  // timing ablation only: stage + classify + roles + scan
   if (ex == 0x123456789ull) a.res[15] = totp;
   return;
@@ -538,6 +543,11 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
     for (uint64_t mm = ro.V; mm && r < kLCap; mm &= mm - 1, ++r) lv[r] = entry((uint32_t)ctz64(mm));
   }
   bk.wave_sync();
+  FAST_STAMP(k, 5);
+#if defined(LSVM_ABL) && LSVM_ABL == 3  // timing ablation only: + run lists
+  if (li[lane] == 0x12345678u) a.res[15] = lv[lane];
+  return;
+#endif
   bool anyfail = false;
   const uint32_t iv = a.indexing_mode > 0 ? 1u : 0u;
   const uint32_t nround = (mx<uint32_t>(nIq, nVq) + kWave - 1) / kWave;  // wave-uniform
@@ -565,12 +575,18 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
     anyfail |= (fi | fv) != 0;
   }
   bk.wave_sync();  // (the failure words and the decoded entries: every lane reads them below)
+  FAST_STAMP(k, 6);
+#if defined(LSVM_ABL) && LSVM_ABL == 4  // timing ablation only: + decode, no look-back
+  if (li[lane] == 0x12345678u || anyfail) a.res[15] = lv[lane];
+  return;
+#endif
   // ---- look-back (wave 0), then the stores
   if (tid < kWave) {
     if (!lean_look_back(a.lean_lb, a.ntiles, k, cnt4, a.gate, sh.base, bk) && tid == 0) sh.flags |= 2u;
   }
   bk.sync();
   if (sh.flags & 2u) return;  // a poisoned tile before this one (block-uniform)
+  FAST_STAMP(k, 7);
   const uint64_t bRows = sh.base[0], bIdx = sh.base[1], bVal = sh.base[2], bW = sh.base[3];
   if (k + 1 == a.ntiles && tid == 0) {  // the last tile publishes the totals
     const uint64_t rows = bRows + nL;
@@ -686,6 +702,7 @@ DA_HDF void tile(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k) {
       row[C_FIELD] = 0;
     }
   }
+  FAST_STAMP(k, 8);
 }
 
 }  // namespace lsvm

@@ -283,14 +283,28 @@ struct PinnedVec {  // page-locked host array, grown on demand (contents not kep
 // hundred MB of HBM (text, workspace, CSR outputs); hipMalloc / hipFree of
 // them cost ~10 ms per parser built and ~10 ms per parser destroyed (hipFree
 // synchronises the device), the same order as parsing a 2 GB file
-// (DESIGN.md 5.2).  Up to kDevCacheBytes per device are kept for reuse
-// (HBM is 288 GB per GPU); blocks past that are freed.
+// (DESIGN.md 5.2).  Up to DMLC_AMD_HBM_CACHE_MB per device (default 8192 MiB,
+// 0: no cache -- every block goes back to hipFree) are kept for reuse (HBM is
+// 288 GB per GPU); blocks past that are freed, and an hipMalloc that fails
+// frees the device's idle blocks and tries once more, so memory the cache
+// holds never causes an out-of-memory error another allocation would not.
 class DevCache {
  public:
-  static constexpr size_t kDevCacheBytes = size_t(8) << 30;
   static DevCache &get() {
     static DevCache *c = new DevCache();  // never destroyed: no HIP call at process exit
     return *c;
+  }
+  // bytes kept per device (DMLC_AMD_HBM_CACHE_MB, read once)
+  static size_t cap_bytes() {
+    static const size_t cap = [] {
+      const char *e = std::getenv("DMLC_AMD_HBM_CACHE_MB");
+      if (!e || !*e) return size_t(8) << 30;
+      char *end = nullptr;
+      const unsigned long long mb = std::strtoull(e, &end, 10);
+      if (end == e || *end) throw dmlc::Error(std::string("DMLC_AMD_HBM_CACHE_MB: not a number: ") + e);
+      return (size_t)mb << 20;
+    }();
+    return cap;
   }
   void *take(int dev, size_t bytes, size_t *got) {
     {
@@ -306,17 +320,38 @@ class DevCache {
       }
     }
     void *p = nullptr;
-    hip_check(hipMalloc(&p, bytes), "hipMalloc");
+    if (hipMalloc(&p, bytes) != hipSuccess) {
+      (void)hipGetLastError();  // (clear the sticky error of the failed call)
+      p = nullptr;
+      if (trim(dev) == 0) hip_check(hipErrorOutOfMemory, "hipMalloc");
+      hip_check(hipMalloc(&p, bytes), "hipMalloc");
+    }
     *got = bytes;
     return p;
   }
   // false: not kept (the caller frees it)
   bool give(int dev, void *p, size_t bytes) {
     std::lock_guard<std::mutex> lk(mu_);
-    if (held_[dev] + bytes > kDevCacheBytes) return false;
+    if (held_[dev] + bytes > cap_bytes()) return false;
     free_[dev].emplace(bytes, p);
     held_[dev] += bytes;
     return true;
+  }
+  // frees the device's idle blocks (the calling thread's current device);
+  // returns the bytes freed
+  size_t trim(int dev) {
+    std::multimap<size_t, void *> fl;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      fl.swap(free_[dev]);
+      held_[dev] = 0;
+    }
+    size_t freed = 0;
+    for (auto &kv : fl) {
+      (void)hipFree(kv.second);
+      freed += kv.first;
+    }
+    return freed;
   }
   // idle non-blocking streams of a device (the calling thread's current one)
   hipStream_t take_stream(int dev) {
@@ -692,6 +727,9 @@ class HipTextParser : public dmlc::Parser<IndexType, DType> {
       } catch (const std::exception &e) {
         b->error = e.what();
         b->fail_at = 0;
+        // kernels queued before the throw may still use this worker's HBM
+        // blocks: drain them before the blocks can go to another worker
+        if (w->stream) (void)hipStreamSynchronize(w->stream);
       }
       {
         std::lock_guard<std::mutex> lk(mu_);

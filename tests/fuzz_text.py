@@ -432,35 +432,38 @@ DIRTY_LINES = ["# synth libsvm shard", "# hdr", "#!", "junk", "@@@", "7 abc 3:4"
                "9 3:nan 4:1", "4 1:inf", "6 NaN(1):2", "1 2:0.5 3:-inf"]
 
 
-def dirty_libsvm(rng, nbytes, rate=0.002, long_frac=0.0, near_tile_end=False):
+def dirty_libsvm(rng, nbytes, rate=0.002, long_frac=0.0, near_tile_end=False, eol=b"\n"):
     """Uniform-grammar libsvm rows (about nbytes) with lines holding bytes
     outside the grammar -- "# header" lines of the next file after InputSplit's
-    '\\n' between files (input_split_base.cc:204-210), words, stray symbols,
+    '\n' between files (input_split_base.cc:204-210), words, stray symbols,
     inf / nan values -- at a share `rate` of the lines; long_frac: share of
     them longer than 256 bytes.  near_tile_end: put dirty lines across and
-    near the 16 KiB single-pass tile ends."""
+    near the 16 KiB single-pass tile ends.  eol: the line end ("\n", "\r\n"
+    or a lone "\r" -- the reference ends a line at either byte,
+    libsvm_parser.h:95)."""
     body = uniform_libsvm(rng, max(1, nbytes // 60), 12).replace(b"\r", b"\n")
     lines = body.split(b"\n")
     out = []
     pos = 0
+    e = len(eol)
     for ln in lines:
         if rng.random() < rate:
             d = DIRTY_LINES[int(rng.integers(0, len(DIRTY_LINES)))].encode()
             if rng.random() < long_frac:
                 d = d + b" " + b"1:2 " * int(rng.integers(70, 120))
             if rng.random() < 0.5:
-                d = b"\n" + d  # the empty line InputSplit leaves between files
+                d = eol + d  # the empty line InputSplit leaves between files
             if near_tile_end:
                 t_end = (pos // 16384 + 1) * 16384
                 gap = t_end - pos - int(rng.integers(-40, 100))
                 if 0 < gap < 400:
-                    out.append(b"1" + b" " * max(0, gap - 2))
-                    pos += len(out[-1]) + 1
+                    out.append(b"1" + b" " * max(0, gap - 1 - e))
+                    pos += len(out[-1]) + e
             out.append(d)
-            pos += len(d) + 1
+            pos += len(d) + e
         out.append(ln)
-        pos += len(ln) + 1
-    return b"\n".join(out) + b"\n"
+        pos += len(ln) + e
+    return eol.join(out) + eol
 
 
 def long_row_libsvm(rng, form, row_kb=(34, 70)):

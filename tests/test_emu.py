@@ -641,14 +641,15 @@ def test_emu_exact_gaps_across_segments():
 def test_emu_fast_dirty_lines_vs_oracle():
     """Lines holding bytes outside the grammar (svm_fast.h dirty_lines): file
     headers mid-chunk, words, symbols, inf / nan values, across and near tile
-    ends, with odd chunkings and long dirty lines (the exact kernels' case):
+    ends, with odd chunkings, CRLF and lone-CR line ends, and long dirty lines (the exact kernels' case):
     the single pass takes the short ones line by line, the rest goes to the
     exact kernels -- whichever path runs, the reference's result."""
     rng = np.random.default_rng(3131)
     paths = {"fast": 0, "exact": 0}
     for it in range(30):
         data = fuzz_text.dirty_libsvm(rng, 70000 if it % 3 else 3000, rate=0.01 if it % 2 else 0.05,
-                                      long_frac=0.3 if it % 5 == 4 else 0.0, near_tile_end=it % 3 == 1)
+                                      long_frac=0.3 if it % 5 == 4 else 0.0, near_tile_end=it % 3 == 1,
+                                      eol=(b"\n", b"\r\n", b"\n", b"\r")[it % 4])
         offs = fuzz_text.random_cuts(rng, data, 5, anywhere=it % 4 == 3)
         kw = {"index_bits": 64} if it % 7 == 1 else ({"indexing_mode": -1} if it % 7 == 2 else {})
         h = _emu_vs_oracle(data, offs, **kw)

@@ -377,7 +377,8 @@ def test_gpu_dirty_lines_vs_oracle(dm):
     paths = {"fast": 0, "exact": 0}
     for it in range(60):
         data = fuzz_text.dirty_libsvm(rng, 120000 if it % 3 else 5000, rate=(0.002, 0.01, 0.05)[it % 3],
-                                      long_frac=0.3 if it % 5 == 4 else 0.0, near_tile_end=it % 3 == 1)
+                                      long_frac=0.3 if it % 5 == 4 else 0.0, near_tile_end=it % 3 == 1,
+                                      eol=(b"\n", b"\r\n", b"\n", b"\r")[it % 4])
         offs = fuzz_text.random_cuts(rng, data, 6, anywhere=it % 4 == 3)
         kw = {"index_bits": 64} if it % 7 == 1 else ({"indexing_mode": -1} if it % 7 == 2 else {})
         h = _gpu_vs_oracle_paths(dm, data, offs, **kw)
