@@ -47,6 +47,9 @@ CONFIGS = {
     # config 2 as a directory of 64 files read by the text InputSplit, each
     # starting with a "# synth libsvm shard" line (per-line fallback, svm_fast.h dirty_lines)
     "libsvm_hdrs_1m_x128": ("libsvm_hdrs", 1 << 20, 128, None),
+    # config 2 with a word (" NA", " feature") or an "<id>:-inf" value on every
+    # eighth row (svm_fast.h dirty_rewrite: the single pass keeps them)
+    "libsvm_dirty_1m_x128": ("libsvm_dirty", 1 << 20, 128, None),
     # grammar variants of configs 2 / 3 (the rates real data hits
     # off the canonical shape)
     "libsvm_nt2_1m_x128": ("libsvm", 1 << 20, 128, None),  # config 2 at the reference's factory nthread = 2
@@ -80,6 +83,7 @@ DESC = {
     "libsvm_qid_1m_x128": "libsvm 1M rows x 128 nnz/row with qid:<row/16> on every row, device-resident",
     "libsvm_cmt_1m_x128": "libsvm 1M rows x 128 nnz/row, a '# row <r>' comment on every row and a header, device-resident",
     "libsvm_hdrs_1m_x128": "libsvm 1M rows x 128 nnz/row as 64 files of 16384 rows, each headed by a '# synth libsvm shard' line, concatenated as InputSplit reads a directory ('\\n' between files), device-resident",
+    "libsvm_dirty_1m_x128": "libsvm 1M rows x 128 nnz/row, every eighth row carrying a word (' NA' / ' feature') or an '<id>:-inf' value mid-row, device-resident",
     "libsvm_nt2_1m_x128": "libsvm 1M rows x 128 nnz/row, each InputSplit chunk cut into nthread=2 ParseBlock ranges (the reference's factory default, text_parser.h:32-35), device-resident",
     "libsvm_im1_1m_x128": "libsvm 1M rows x 128 nnz/row, indexing_mode=-1 (per-range 1-based detection), device-resident",
     "libsvm_1b_im1_1m_x128": "libsvm 1M rows x 128 nnz/row with 1-based ids, indexing_mode=-1 (every range detected 1-based and shifted), device-resident",
@@ -92,12 +96,13 @@ DESC = {
 }
 SYNTH = {"libsvm": synth.LIBSVM, "csv": synth.CSV, "libfm": synth.LIBFM, "libsvm_qid": synth.LIBSVM_QID,
          "libsvm_cmt": synth.LIBSVM_CMT, "csv_sp": synth.CSV_SP, "libsvm_1b": synth.LIBSVM_1B,
-         "csv_nan": synth.CSV_NAN, "libsvm_hdrs": synth.LIBSVM_HDRS}
+         "csv_nan": synth.CSV_NAN, "libsvm_hdrs": synth.LIBSVM_HDRS, "libsvm_dirty": synth.LIBSVM_DIRTY}
 # the arithmetic the path computes in (values decoded to f32 through the
 # reference's f64 fraction divide; indices / fields as u32)
 DTYPE = {"libsvm": "f32 values / u32 index", "libsvm_1b": "f32 values / u32 index",
          "libsvm_qid": "f32 values / u32 index / u64 qid",
          "libsvm_cmt": "f32 values / u32 index", "libsvm_hdrs": "f32 values / u32 index",
+         "libsvm_dirty": "f32 values / u32 index",
          "csv": "f32 values", "csv_sp": "f32 values", "csv_nan": "f32 values",
          "libfm": "f32 values / u32 index / u32 field"}
 
@@ -297,7 +302,8 @@ def main():
     d_text = torch.from_numpy(text).to(dev)
     d_starts = torch.from_numpy(starts).to(dev)
     nbytes = int(text.size)
-    pfmt = {"libsvm_qid": "libsvm", "libsvm_cmt": "libsvm", "libsvm_1b": "libsvm", "libsvm_hdrs": "libsvm", "csv_sp": "csv",
+    pfmt = {"libsvm_qid": "libsvm", "libsvm_cmt": "libsvm", "libsvm_1b": "libsvm", "libsvm_hdrs": "libsvm",
+            "libsvm_dirty": "libsvm", "csv_sp": "csv",
             "csv_nan": "csv"}.get(fmt, fmt)
     pkw = dict(PARAMS.get(args.config, {}))
     if pfmt == "csv":

@@ -98,16 +98,26 @@ DA_HD bool is_qid_letter(uint32_t b) { return b == 'q' || b == 'i' || b == 'd'; 
 // four bytes there (one word read, `wd`) must be "qid:" -- which also bounds
 // the run to the token's three letters.  (Round 2 read five bytes per letter.)
 constexpr uint32_t kQidWord = 0x3A646971u;  // "qid:" little-endian
+// stray (optional): the letters of runs that are no "qid:" token -- bytes
+// outside the grammar, which the dirty pass (dirty_rewrite) takes like any
+// other; without it such letters fail the check.  A "qid:" token not followed
+// by a digit always fails it (atoll's whitespace and sign, :126).
 template <class At, class Wd>
-DA_HD bool qid_clean(uint64_t P, uint64_t *n, uint64_t *c, bool lead, At at, Wd wd) {
+DA_HD bool qid_clean(uint64_t P, uint64_t *n, uint64_t *c, bool lead, At at, Wd wd, uint64_t *stray = nullptr) {
   const uint64_t X = *n & *c;
   bool ok = true;
+  uint64_t sx = 0;
   for (uint64_t m = X & ~(X << 1); m; m &= m - 1) {
     const uint64_t x = P + ctz64(m);
     const uint32_t b = at(x);
     const uint64_t s0 = x - (b == 'q' ? 0u : b == 'i' ? 1u : 2u);
-    ok = ok && wd(s0) == kQidWord;
+    if (wd(s0) != kQidWord) {
+      const uint64_t lb = m & (0 - m);
+      sx |= X & ((X + lb) ^ X);  // the letter run from this bit
+    }
   }
+  if (stray) *stray = sx;
+  else ok = sx == 0;
   uint64_t qc = 0;
   for (uint64_t m = *c & ~X & ((X << 1) | (lead ? 1u : 0u)); m; m &= m - 1) {
     const uint64_t x = P + ctz64(m);
@@ -952,9 +962,14 @@ DA_HDF uint32_t commit_seg(const Tile &t, Shared &sh, int seg, At at, bool first
   const uint64_t P0 = t.tlo + (uint64_t)seg * kSegB;
   if ((m.n & m.c) || ((m.c & 1) && P0 > 0 && is_qid_letter(at(P0 - 1)))) {  // letters: "qid:" tokens
     auto wd = [&](uint64_t p) -> uint32_t { return text_word(t, p, at); };
-    if (FM || !qid_clean(P0, &m.n, &m.c, P0 > 0 && is_qid_letter(at(P0 - 1)), at, wd)) {
+    uint64_t stray = 0;  // letters of no "qid:" token: bytes outside the grammar (the digit plane marks them)
+    if (FM || !qid_clean(P0, &m.n, &m.c, P0 > 0 && is_qid_letter(at(P0 - 1)), at, wd, &stray)) {
       bad = 1;
       if (!FM && first) atomic_or_u64(&sh.qfail[seg / kWave], 1ull << (seg % kWave));
+    }
+    if (stray) {
+      m.g |= stray;
+      m.bad = 1;
     }
   }
   sh.gw[2 * seg] = (uint32_t)m.g;
@@ -997,7 +1012,12 @@ DA_HDF uint32_t classify_tile(const Tile &t, Shared &sh, int tid, At at, bool fi
     if (!FM && ((bn & bc) || (bc & 1))) {  // the bytes' owner tile checks them; here only their planes
       const bool lead = is_qid_letter(at(P0 - 1));
       auto wd = [&](uint64_t p) -> uint32_t { return text_word(t, p, at); };
-      if ((bn & bc) || lead) (void)qid_clean(P0, &bn, &bc, lead, at, wd);
+      uint64_t stray = 0;
+      if ((bn & bc) || lead) (void)qid_clean(P0, &bn, &bc, lead, at, wd, &stray);
+      if (stray) {  // letters of no token: outside the grammar (dirty_lines / dirty_rewrite)
+        if (first) sh.hashy = 1;
+        atomic_or_u64(&sh.prebad, stray << (4 * tid));
+      }
     }
     atomic_or_u64(&sh.u.m.d[0], (uint64_t)b.d << (4 * tid));
     atomic_or_u64(&sh.u.m.n[0], bn << (4 * tid));
@@ -1316,6 +1336,165 @@ DA_HDF uint32_t dirty_lines(const Tile &t, Shared &sh, uint32_t bad, BK &bk, At 
   return bad;
 }
 
+// ---- dirty rewrite (round 6): lines holding bytes outside the grammar at any
+// length and density, without a walk.  Outside a "qid:" token, a byte X that
+// is no digitchar, blank, newline or ':' acts in ParseBlock exactly like a
+// blank (ParsePair skips it on the way to a run, strtonum.h:671-673 and
+// :686-688; IgnoreCommentAndBlank stops at it, libsvm_parser.h:67-83 -- the
+// comment pass already read it so) except in three places:
+//   * a ':' pairs a value only when it is the first non-blank byte after the
+//     run before it (:683-687) -- "5 x:3" is two indices, "5 :x 3" a pair;
+//   * ParseFloat reads on past a sign into "inf" / "nan(...)" letters
+//     (strtonum.h:133-175): a run of one sign followed by i / n;
+//   * "qid:" after the label (libsvm_parser.h:119-132) -- a tile holding a
+//     qid marker declines (the walk, dirty_lines, takes it).
+// So the tile blanks every X byte and every ':' that is not the first
+// non-blank byte after a run end in its staged text and classifies the
+// changed segments again -- the role arithmetic then reads the reference's
+// pairs.  The letter after a one-sign run ("-inf") becomes an 'e' instead: the
+// run stays where it was, and the window decoder, seeing an exponent, hands
+// the number to the byte decoder, which reads the text in HBM.  The first non-blank
+// byte after each run end is a carry chain through the blanks: the gap
+// starts E (a byte after a digitchar) added into the blank plane land on it.
+// A segment whose result depends on the gap state at its start takes it from
+// the segment before (through all-blank segments); a tile whose answer lies
+// before its pre-halo declines.  Returns the tile's flags as dirty_lines;
+// *took: false when the tile declined (block-uniform).
+constexpr uint32_t kDeclined = 1u << 16;  // Shared::hashy: dirty_rewrite declined the tile
+template <class BK, class At>
+DA_HDF uint32_t dirty_rewrite(const Tile &t, Shared &sh, uint32_t bad, BK &bk, At at, uint32_t k, bool *took) {
+  (void)k;
+  const int tid = bk.tid();
+  const uint32_t lane = (uint32_t)tid & (kWave - 1);
+  const uint64_t n = t.a->n;
+  const uint64_t P = t.tlo + (uint64_t)tid * kSegB;
+  const bool pre = t.tlo > 0;  // slot 0 holds the 64 bytes before the tile
+  // outside bytes of slot s (0: the pre-halo)
+  auto x_of = [&](int s) -> uint64_t { return s == 0 ? (pre ? sh.prebad : 0ull) : outside_mask(t, sh, s - 1); };
+  // the gap state after slot s: 1 when its last non-blank byte is a
+  // digitchar before its last byte (a gap with blanks only is open at its
+  // end); through all-blank slots to the pre-halo, *unk past it
+  auto pend_after = [&](int s, bool *unk) -> uint32_t {
+    for (; s >= 0; --s) {
+      if (s == 0 && !pre) return 0u;
+      const uint64_t d = sh.u.m.d[s];
+      const uint64_t nb = d | sh.u.m.n[s] | sh.u.m.c[s] | x_of(s);
+      if (nb) {
+        const int hb = 63 - clz64(nb);
+        return ((d >> hb) & 1u) && hb < 63 ? 1u : 0u;
+      }
+    }
+    *unk = true;
+    return 0u;
+  };
+  // bytes of slot s to blank, for a gap state pin at its start and the
+  // digitchar bit before it
+  auto rewrite = [&](int s, uint64_t valid, uint32_t pin, uint64_t dprev) -> uint64_t {
+    const uint64_t d = sh.u.m.d[s], c = sh.u.m.c[s], X = x_of(s) & valid;
+    const uint64_t bl = ~(d | sh.u.m.n[s] | c | X) & valid;
+    const uint64_t E = ~d & ((d << 1) | dprev) & valid;  // gap starts
+    uint32_t co;
+    const uint64_t land = (add_carry(bl, E & bl, pin, &co) | E) & ~bl & valid;  // first non-blank after a run end
+    return X | (c & ~land);
+  };
+  uint32_t decline = 0;
+  // a qid marker anywhere (the walk takes qid lines), and the rewrite of my segment
+  uint64_t R = 0;
+  if (P < n) {
+    const int s = tid + 1;
+    if (sh.u.m.n[s] & sh.u.m.c[s]) decline = 1;
+    const uint64_t valid = n - P >= 64 ? ~0ull : (1ull << (n - P)) - 1;
+    const uint64_t dprev = (sh.u.m.d[s - 1] >> 63) & 1u;
+    const uint64_t r0 = rewrite(s, valid, 0u, dprev), r1 = rewrite(s, valid, 1u, dprev);
+    R = r0;
+    if (r0 != r1) {  // the gap state at my start decides: from the segments before
+      bool unk = false;
+      if (pend_after(s - 1, &unk)) R = r1;
+      if (unk) decline = 1;
+    }
+  }
+  // the pre-halo (thread 0): the byte before it read from HBM; the gap state
+  // at its start is not staged -- it must not matter
+  uint64_t Rpre = 0;
+  if (tid == 0 && pre) {
+    if (sh.u.m.n[0] & sh.u.m.c[0]) decline = 1;
+    const uint64_t dp = t.tlo > (uint64_t)kPre && is_digitchar(at(t.tlo - kPre - 1)) ? 1u : 0u;
+    Rpre = rewrite(0, ~0ull, 0u, dp);
+    if (Rpre != rewrite(0, ~0ull, 1u, dp)) decline = 1;
+  }
+  if (decline) atomic_or_u32(&sh.hashy, kDeclined);
+  bk.sync();
+  if (sh.hashy & kDeclined) {  // block-uniform: the walk decides
+    *took = false;
+    return bad;
+  }
+  *took = true;
+  // the letters after one-sign runs among R (x: the byte's position, bit:
+  // its bit; d2: the digitchar planes' bits before it, `bit`-relative): 'e'
+  auto inf_marks = [&](uint64_t P0, uint64_t m, uint64_t dcur, uint64_t dbefore) -> uint64_t {
+    uint64_t em = 0;
+    for (uint64_t mm = m & ((dcur << 1) | (dbefore >> 63)); mm; mm &= mm - 1) {  // bytes right after a run
+      const int b = ctz64(mm);
+      const uint64_t x = P0 + (uint64_t)b;
+      const bool d2 = b >= 2 ? ((dcur >> (b - 2)) & 1u) : ((dbefore >> (62 + b)) & 1u);
+      const uint32_t s0 = at(x - 1), l = at(x) | 0x20u;
+      if (!d2 && (s0 == '+' || s0 == '-') && (l == 'i' || l == 'n')) em |= 1ull << b;
+    }
+    return em;
+  };
+  // R into the staged bytes (a word at a time): blanks, 'e' at em
+  auto blank_words = [&](uint8_t *base, uint64_t m, uint64_t em) {
+    uint32_t *w = reinterpret_cast<uint32_t *>(base);
+    for (uint64_t mm = m; mm;) {
+      const int q = ctz64(mm) >> 2;
+      const uint32_t nib = (uint32_t)(m >> (4 * q)) & 0xFu, eib = (uint32_t)(em >> (4 * q)) & 0xFu;
+      const uint32_t bm = ((nib * 0x00204081u) & 0x01010101u) * 0xFFu;
+      const uint32_t be = ((eib * 0x00204081u) & 0x01010101u) * 0xFFu;
+      w[q] = (w[q] & ~bm) | (0x20202020u & bm & ~be) | (0x65656565u & be);
+      mm &= ~(0xFull << (4 * q));
+    }
+  };
+  if (R) {
+    const int s = tid + 1;
+    blank_words(sh.c.text + kPre + tid * kSegB, R, inf_marks(P, R & x_of(s), sh.u.m.d[s], sh.u.m.d[s - 1]));
+  }
+  // the pre-halo: its bytes rewritten, its planes again (classify_tile part
+  // 2); the post-halo: its outside bytes rewritten (the last runs' windows),
+  // its digit word again (part 4)
+  uint32_t parts = 0;
+  if (tid == 0 && Rpre) {
+    uint64_t dp = 0;  // the digitchar bits of the two bytes before the pre-halo, as bits 62-63
+    for (uint64_t i = 1; i <= 2; ++i)
+      if (t.tlo >= (uint64_t)kPre + i && is_digitchar(at(t.tlo - kPre - i))) dp |= 1ull << (64 - i);
+    blank_words(sh.c.text, Rpre, inf_marks(t.tlo - kPre, Rpre & x_of(0), sh.u.m.d[0], dp));
+    parts |= 2u;
+  }
+  const uint64_t shi = mn<uint64_t>(t.tlo + kTile + kPost, n);
+  if (tid >= kFThreads - kWave) {
+    // (read from HBM: the bytes before may be rewritten meanwhile)
+    for (uint64_t x = t.thi + lane; x < shi; x += kWave) {
+      const uint32_t b = gbyte(t.a->text, x);
+      if (!is_digitchar(b) && !is_blank(b) && !is_nl(b) && b != ':') {
+        const uint32_t s0 = gbyte(t.a->text, x - 1), l = b | 0x20u;
+        const bool e = (s0 == '+' || s0 == '-') && !is_digitchar(gbyte(t.a->text, x - 2)) && (l == 'i' || l == 'n');
+        sh.c.text[x - t.tlo + kPre] = e ? 'e' : ' ';
+        parts |= 4u;
+      }
+    }
+  }
+  const uint64_t pm = bk.ballot((parts & 2u) != 0), qm = bk.ballot((parts & 4u) != 0);
+  parts = (pm ? 2u : 0u) | (qm ? 4u : 0u);
+  if (parts) atomic_or_u32(&sh.hashy, parts << 8);
+  bk.sync();
+  parts = (sh.hashy >> 8) & 6u;
+  if (tid == 0 && (parts & 2u)) {
+    sh.u.m.d[0] = sh.u.m.n[0] = sh.u.m.c[0] = 0;
+    sh.prebad = 0;
+  }
+  bk.sync();
+  return reclassify_blanked(t, sh, bad, R != 0, parts, bk, at);
+}
+
 // After the tile's aggregate is published (MODE 2, before the run lists):
 // the walked lines' bytes back into the staged text and the digit plane, for
 // the index windows.  (Done before the roles, its global round trip sat on
@@ -1570,7 +1749,10 @@ DA_HDF uint32_t tile_p(const FastSvmArgs &a, Shared &sh, BK &bk, uint32_t k, Sta
     }
     if (nseg > 2u || sh.dgate) bad = comments_reclassify(t, sh, bad, bk, k);
     FAST_STAMP(k, 12);
-    bad = dirty_lines(t, sh, bad, bk, at, k);  // lines still holding bytes outside the grammar
+    // lines still holding bytes outside the grammar: rewritten, else walked
+    bool took = false;
+    bad = dirty_rewrite(t, sh, bad, bk, at, k, &took);
+    if (!took) bad = dirty_lines(t, sh, bad, bk, at, k);
     FAST_STAMP(k, 14);
   }
   if (tid == 0) bad |= sh.c.toomany;

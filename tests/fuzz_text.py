@@ -466,6 +466,67 @@ def dirty_libsvm(rng, nbytes, rate=0.002, long_frac=0.0, near_tile_end=False, eo
     return eol.join(out) + eol
 
 
+# Dirty tokens inside rows (round 6, svm_fast.h dirty_rewrite): words (with
+# digitchar letters e/E and the qid letters q / i / d among them), symbols,
+# bytes >= 0x80, a vertical tab, an unreachable '#' (behind a non-blank byte:
+# no comment, libsvm_parser.h:67-83), a ':' behind a non-blank
+# byte -- all of which ParsePair skips like blanks except where they stand
+# between a run and its ':' (strtonum.h:683-687) -- and ParseFloat's inf /
+# nan forms after a sign (strtonum.h:133-175).  (An unsigned "nan" value
+# is skipped to the next run, "a:b:c" -- the exact kernels take that.)
+ROW_TOKENS = [b"NA", b"null", b"did", b"x", b"~", b"@@", b"qi", b"dq", b"x#y", b"\x0b", b"\xc3\xa9t\xc3\xa9", b"!",
+              b"n/a", b"q:", b"::"]
+# tokens holding digitchar runs of their own (read as index-only ids: a block
+# mixing them with valued pairs fails the reference's RowBlock CHECK,
+# row_block.h:178 -- the tests then compare the failure)
+RUN_TOKENS = [b"feature", b"note", b"Eq", b"id:4", b"x:3", b"x#5", b"(1)", b"idx=7"]
+VALUE_TOKENS = [b"-inf", b"+nan", b"-Infinity", b"-nan(7)", b"+INF", b"-x", b"+", b"-n"]
+
+
+def dirty_rows_libsvm(rng, nrows, width, rate=0.125, eol=b"\n", near_tile_end=False, runs=False):
+    """libsvm rows of `width` pairs (ids increasing, "%.9g" values) where a
+    share `rate` of the rows carries 1-3 dirty tokens: a word between pairs,
+    an inf / nan value ("3:-inf") or label; with `runs`, also words holding
+    digitchar runs and words glued to an index ("5x:0.3": index-only pairs).  No qid tokens, no dangling ':' and no
+    "a:b:c" chains, so the single pass keeps every such input
+    (dirty_rewrite) -- the tests check that it does and that the result is
+    the reference's."""
+    out = []
+    pos = 0
+    for r in range(nrows):
+        ids = np.cumsum(rng.integers(1, 17, size=width)) - 1
+        vals = rng.random(width).astype(np.float32)
+        toks = [b"%d:%.9g" % (int(i), float(v)) for i, v in zip(ids, vals)]
+        label = b"%d" % int(rng.integers(0, 2))
+        if rng.random() < rate:
+            for _ in range(int(rng.integers(1, 4))):
+                kind = rng.random()
+                j = int(rng.integers(0, width)) if width else 0
+                pool = ROW_TOKENS + RUN_TOKENS if runs else ROW_TOKENS
+                if kind < 0.45 or width == 0:
+                    toks.insert(j, pool[int(rng.integers(0, len(pool)))])
+                elif kind < 0.65 and runs:
+                    t = pool[int(rng.integers(0, len(pool)))].split(b":")[0]
+                    if b":" in toks[j]:  # (not a token inserted before)
+                        toks[j] = b"%s%s:%s" % (toks[j].split(b":")[0], t, toks[j].split(b":")[1])
+                elif kind < 0.95:
+                    if b":" in toks[j]:
+                        toks[j] = b"%s:%s" % (toks[j].split(b":")[0], VALUE_TOKENS[int(rng.integers(0, len(VALUE_TOKENS)))])
+                else:
+                    label = VALUE_TOKENS[int(rng.integers(0, len(VALUE_TOKENS)))]
+        sep = b"\t" if rng.random() < 0.05 else b" "
+        line = label + b"".join(sep + t for t in toks)
+        if near_tile_end and rng.random() < 0.3:
+            t_end = (pos // 16384 + 1) * 16384
+            gap = t_end - pos - int(rng.integers(0, 64))
+            if 0 < gap < 200:
+                out.append(b"1" + b" " * max(0, gap - 1 - len(eol)))
+                pos += len(out[-1]) + len(eol)
+        out.append(line)
+        pos += len(line) + len(eol)
+    return eol.join(out) + eol
+
+
 def long_row_libsvm(rng, form, row_kb=(34, 70)):
     """Short rows around one to three rows longer than four exact windows
     (> 32 KiB), so that at exact tile_bytes=4096 (three recorded windows per

@@ -54,6 +54,13 @@ CONFIGS = {
     "csv_label0_1m_x256": (synth.CSV, po.CSV, 1 << 20, 256, 0),
     "csv_lw_1m_x256": (synth.CSV, po.CSV, 1 << 20, 256, 0),
     "libfm_exact_1m_x64": (synth.LIBFM, po.LIBFM, 1 << 20, 64, 0),
+    # round 6: integer DTypes (glibc strtoll, csv_parser.h:99-105) and 64-bit
+    # indices (data.cc:214-221's Parser<uint64_t, .> registrations)
+    "csv_i32_1m_x256": (synth.CSV, po.CSV, 1 << 20, 256, 0),
+    "csv_sp_i64_1m_x256": (synth.CSV_SP, po.CSV, 1 << 20, 256, 0),
+    "libsvm_w64_1m_x128": (synth.LIBSVM, po.LIBSVM, 1 << 20, 128, 0),
+    # round 6: words and -inf values on every eighth row (svm_fast.h dirty_rewrite)
+    "libsvm_dirty_1m_x128": (synth.LIBSVM_DIRTY, po.LIBSVM, 1 << 20, 128, 0),
 }
 for _r in range(8):  # config 5: bench.py's rank r shard of 32M x 64 (4M rows from row r * 4M)
     CONFIGS["libsvm_32m_x64_part%d" % _r] = (synth.LIBSVM, po.LIBSVM, 4 << 20, 64, _r * (4 << 20))
@@ -66,6 +73,29 @@ PARAMS = {
     "csv_label0_1m_x256": {"label_column": 0},
     "csv_lw_1m_x256": {"label_column": 3, "weight_column": 7},
 }
+# value DType and index width per config (the reference's Parser<IndexType,
+# DType> instantiation; default uint32_t / float)
+TYPES = {"csv_i32_1m_x256": ("i32", 32), "csv_sp_i64_1m_x256": ("i64", 32), "libsvm_w64_1m_x128": ("f32", 64)}
+
+
+def ref_kw(name):
+    """The reference-side arguments of a config (pyoracle.params)."""
+    kw = dict(PARAMS.get(name, {}))
+    if name in TYPES:
+        vt, ib = TYPES[name]
+        kw.update(value_kind={"f32": po.F32, "i32": po.I32, "i64": po.I64}[vt], index_bits=ib)
+    return kw
+
+
+def gpu_kw(name):
+    """The GPU-side arguments of a config (dmlc_amd.make_params)."""
+    kw = dict(PARAMS.get(name, {}))
+    if name in TYPES:
+        vt, ib = TYPES[name]
+        kw.update(value_type=vt, index_bits=ib)
+    return kw
+
+
 FLAGS = {"libsvm_exact_1m_x128": ("exact", 1), "csv_exact_1m_x256": ("exact", 1), "libfm_exact_1m_x64": ("exact", 1)}
 
 
@@ -111,7 +141,7 @@ def parse_batch(chunks, ofmt, kw):
 
 def run(name):
     sfmt, ofmt, rows, width, row0 = CONFIGS[name]
-    kw = PARAMS.get(name, {})
+    kw = ref_kw(name)
     block_rows = max(1, (16 << 20) // (width * 16))
     hs = {k: hashlib.sha256() for k in ARRAYS}
     sizes = {k: 0 for k in ARRAYS}
@@ -122,6 +152,8 @@ def run(name):
 
     def consume(out):
         nonlocal base
+        if out["status"] != 0:  # the reference refused the input: no fixture
+            raise SystemExit("%s: reference error %s" % (name, out["msg"]))
         off = np.asarray(out["offset"], dtype=np.uint64)
         if sizes["offset"]:
             off = off[1:]  # the batch's leading 0 is the previous batch's closing offset
@@ -157,7 +189,7 @@ def run(name):
     res = {"format": {po.LIBSVM: "libsvm", po.CSV: "csv", po.LIBFM: "libfm"}[ofmt], "rows": rows,
            "width": width, "row0": row0, "seed": 1, "input_bytes": nbytes, "chunks": nchunks,
            "first_chunk_sha256": first_chunk_sha, "reference": "oracle/_ref (genuine ParseBlock, nthread %d)" % kw.get("nthread", 1),
-           "params": kw,
+           "params": PARAMS.get(name, {}), "types": TYPES.get(name, ("f32", 32)),
            "sha256": {k: hs[k].hexdigest() for k in ARRAYS}, "sizes": sizes}
     print("%s: %.2f GB, %d chunks, %d rows, %d entries in %.0f s" % (name, nbytes / 1e9, nchunks,
                                                                         sizes["offset"] - 1, sizes["index"],

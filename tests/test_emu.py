@@ -657,6 +657,26 @@ def test_emu_fast_dirty_lines_vs_oracle():
     assert paths["fast"] >= 8 and paths["exact"] >= 3, paths
 
 
+def test_emu_fast_dirty_rows_stay_single_pass():
+    """Rows carrying words, symbols, bytes >= 0x80, a ':' behind a non-blank
+    byte, and inf / nan values and labels (fuzz_text.dirty_rows_libsvm) at
+    1/8, 1/2 and every row, long rows across tile ends, CRLF / lone-CR line
+    ends, odd chunkings, 64-bit ids and indexing_mode -1 / 1: the single pass
+    keeps every input (svm_fast.h dirty_rewrite -- no line walk, no exact
+    path) and its result is the reference's."""
+    rng = np.random.default_rng(6061)
+    for it in range(18):
+        width = int(rng.integers(4, 90))
+        data = fuzz_text.dirty_rows_libsvm(rng, max(4, 60000 // (width * 16 + 4)), width,
+                                           rate=(0.125, 0.5, 1.0)[it % 3], eol=(b"\n", b"\r\n", b"\r")[it % 3 == 1 and 1 or (2 if it % 5 == 4 else 0)],
+                                           near_tile_end=it % 2 == 1, runs=it % 3 == 2)
+        offs = fuzz_text.random_cuts(rng, data, 4, anywhere=False)
+        kw = {"index_bits": 64} if it % 4 == 1 else ({"indexing_mode": -1} if it % 4 == 2 else
+                                                      ({"indexing_mode": 1} if it % 4 == 3 else {}))
+        h = _emu_vs_oracle(data, offs, **kw)
+        assert h["path"] == "fast", (it, kw)
+
+
 def test_emu_fast_file_headers():
     """Files with a "# ..." first line concatenated the way InputSplit reads a
     directory ('\\n' between files, input_split_base.cc:204-210): headers

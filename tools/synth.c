@@ -26,6 +26,11 @@
  *    (input_split_base.cc:204-210), so every header after the first sits
  *    mid-chunk after an empty line, where the reference parses it as a line
  *    (libsvm_parser.h:91-104; no digitchar in it: an empty line).
+ *  libsvm with dirty rows (fmt 9): the libsvm row, and on every eighth row
+ *    (r % 8 == 3) mid-row either a missing-value word " NA" / " n/a" or an
+ *    infinite value "<id>:-inf" -- bytes outside the uniform grammar that
+ *    ParsePair skips (strtonum.h:667-703) and ParseFloat's inf
+ *    (strtonum.h:133-175).
  *  CSV with missing values (fmt 7): the CSV row with 0.1 % of its fields
  *    "nan" (numpy.savetxt's missing value; ParseFloat's NAN branch,
  *    strtonum.h:133-175), and a UTF-8 BOM at the head of the file
@@ -48,7 +53,7 @@ static inline uint64_t row_state(uint64_t seed, uint64_t r) {
   return s;
 }
 
-static size_t fmt_libsvm_row(char *o, uint64_t seed, uint64_t r, int K, int qid, int cmt, int one_based) {
+static size_t fmt_libsvm_row(char *o, uint64_t seed, uint64_t r, int K, int qid, int cmt, int one_based, int dirty) {
   uint64_t s = row_state(seed, r);
   char *p = o;
   *p++ = (char)('0' + (sm64(&s) & 1));
@@ -59,6 +64,15 @@ static size_t fmt_libsvm_row(char *o, uint64_t seed, uint64_t r, int K, int qid,
     uint64_t gap = 1 + (x & 15);
     id = j == 0 ? gap - 1 + (uint64_t)one_based : id + gap;
     float v = (float)(x >> 40) * (1.0f / 16777216.0f);
+    /* fmt 9: every eighth row carries a word or an infinite value mid-row */
+    if (dirty && (r & 7) == 3 && j == K / 2) {
+      const int kind = (int)((r >> 3) % 3);
+      if (kind == 1) {
+        p += sprintf(p, " %llu:-inf", (unsigned long long)id);
+        continue;
+      }
+      p += sprintf(p, kind == 0 ? " NA" : " n/a");
+    }
     p += sprintf(p, " %llu:%.9g", (unsigned long long)id, (double)v);
   }
   if (cmt) p += sprintf(p, " # row %llu", (unsigned long long)r);
@@ -97,7 +111,7 @@ static size_t fmt_csv_row(char *o, uint64_t seed, uint64_t r, int C, int blank, 
 
 /* upper bound on the bytes of `nrows` rows */
 size_t synth_bound(int fmt, uint64_t nrows, int width) {
-  return fmt == 0 || fmt == 3 || fmt == 4 || fmt == 6 || fmt == 8 ? nrows * (size_t)(2 + 28 + width * 26) + 32
+  return fmt == 0 || fmt == 3 || fmt == 4 || fmt == 6 || fmt == 8 || fmt == 9 ? nrows * (size_t)(2 + 28 + width * 26) + 32
                   : fmt == 2 ? nrows * (size_t)(2 + width * 30) : nrows * (size_t)(width * 19 + 2) + 3;
 }
 
@@ -123,8 +137,8 @@ size_t synth_rows(int fmt, uint64_t row0, uint64_t nrows, int width, uint64_t se
       if (fmt == 7 && row0 + r == 0) n += (size_t)sprintf(buf + n, "\xEF\xBB\xBF");
       if (fmt == 8 && (row0 + r) % 16384 == 0)
         n += (size_t)sprintf(buf + n, row0 + r ? "\n# synth libsvm shard\n" : "# synth libsvm shard\n");
-      n += fmt == 0 || fmt == 3 || fmt == 4 || fmt == 6 || fmt == 8
-               ? fmt_libsvm_row(buf + n, seed, row0 + r, width, fmt == 3, fmt == 4, fmt == 6)
+      n += fmt == 0 || fmt == 3 || fmt == 4 || fmt == 6 || fmt == 8 || fmt == 9
+               ? fmt_libsvm_row(buf + n, seed, row0 + r, width, fmt == 3, fmt == 4, fmt == 6, fmt == 9)
                     : fmt == 2 ? fmt_libfm_row(buf + n, seed, row0 + r, width)
                                : fmt_csv_row(buf + n, seed, row0 + r, width, fmt == 5, fmt == 7);
     }

@@ -18,6 +18,7 @@ fmt, rows, width, kind = {"libsvm": ("libsvm", 1 << 20, 128, synth.LIBSVM), "csv
                           "qid": ("libsvm", 1 << 20, 128, synth.LIBSVM_QID),
                           "cmt": ("libsvm", 1 << 20, 128, synth.LIBSVM_CMT),
                           "hdrs": ("libsvm", 1 << 20, 128, synth.LIBSVM_HDRS),
+                          "dirty": ("libsvm", 1 << 20, 128, synth.LIBSVM_DIRTY),
                           "libfm": ("libfm", 1 << 20, 64, synth.LIBFM),
                           "csv_nan": ("csv", 1 << 20, 256, synth.CSV_NAN),
                           "exact": ("libsvm", 1 << 20, 128, synth.LIBSVM),
