@@ -59,6 +59,7 @@ CONFIGS = {
     "csv_sp_1m_x256": ("csv_sp", 1 << 20, 256, None),      # config 3 with ", " between values
     "csv_hdr_1m_x256": ("csv", 1 << 20, 256, None),        # config 3 behind a header row of column names
     "csv_nan_1m_x256": ("csv_nan", 1 << 20, 256, None),    # config 3 with 0.1 % "nan" fields and a BOM at the head
+    "csv_dirty_1m_x256": ("csv_nanp", 1 << 20, 256, None),  # config 3 with a "NaN(x)" field on every 64th row
     # the exact kernels (the path input outside the single-pass grammar takes:
     # inf / nan tokens, BOM lines, '#' lines after a range's first line, qid
     # mixes) on configs 2 / 3, forced with DMLC_AMD_FLAG_EXACT
@@ -91,19 +92,21 @@ DESC = {
     "csv_sp_1m_x256": "CSV dense 1M rows x 256 float cols, ', ' separators, device-resident",
     "csv_hdr_1m_x256": "CSV dense 1M rows x 256 float cols behind a header row of column names, device-resident",
     "csv_nan_1m_x256": "CSV dense 1M rows x 256 float cols, 0.1% of fields \"nan\", UTF-8 BOM at the file head, device-resident",
+    "csv_dirty_1m_x256": "CSV dense 1M rows x 256 float cols, every 64th row's middle field \"NaN(x)\" (ParseFloat's NAN(chars) form), device-resident",
     "libsvm_exact_1m_x128": "libsvm 1M rows x 128 nnz/row on the exact kernels (DMLC_AMD_FLAG_EXACT), device-resident",
     "csv_exact_1m_x256": "CSV dense 1M rows x 256 float cols on the exact kernels (DMLC_AMD_FLAG_EXACT), device-resident",
 }
 SYNTH = {"libsvm": synth.LIBSVM, "csv": synth.CSV, "libfm": synth.LIBFM, "libsvm_qid": synth.LIBSVM_QID,
          "libsvm_cmt": synth.LIBSVM_CMT, "csv_sp": synth.CSV_SP, "libsvm_1b": synth.LIBSVM_1B,
-         "csv_nan": synth.CSV_NAN, "libsvm_hdrs": synth.LIBSVM_HDRS, "libsvm_dirty": synth.LIBSVM_DIRTY}
+         "csv_nan": synth.CSV_NAN, "libsvm_hdrs": synth.LIBSVM_HDRS, "libsvm_dirty": synth.LIBSVM_DIRTY,
+         "csv_nanp": synth.CSV_NANP}
 # the arithmetic the path computes in (values decoded to f32 through the
 # reference's f64 fraction divide; indices / fields as u32)
 DTYPE = {"libsvm": "f32 values / u32 index", "libsvm_1b": "f32 values / u32 index",
          "libsvm_qid": "f32 values / u32 index / u64 qid",
          "libsvm_cmt": "f32 values / u32 index", "libsvm_hdrs": "f32 values / u32 index",
          "libsvm_dirty": "f32 values / u32 index",
-         "csv": "f32 values", "csv_sp": "f32 values", "csv_nan": "f32 values",
+         "csv": "f32 values", "csv_sp": "f32 values", "csv_nan": "f32 values", "csv_nanp": "f32 values",
          "libfm": "f32 values / u32 index / u32 field"}
 
 
@@ -303,7 +306,7 @@ def main():
     d_starts = torch.from_numpy(starts).to(dev)
     nbytes = int(text.size)
     pfmt = {"libsvm_qid": "libsvm", "libsvm_cmt": "libsvm", "libsvm_1b": "libsvm", "libsvm_hdrs": "libsvm",
-            "libsvm_dirty": "libsvm", "csv_sp": "csv",
+            "libsvm_dirty": "libsvm", "csv_sp": "csv", "csv_nanp": "csv",
             "csv_nan": "csv"}.get(fmt, fmt)
     pkw = dict(PARAMS.get(args.config, {}))
     if pfmt == "csv":

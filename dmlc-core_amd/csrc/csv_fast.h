@@ -424,6 +424,16 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
             bool cs = x0 <= sh.c.cfloor && sh.c.cfloor < P;  // a chunk (and row) starts inside the run
             for (uint32_t i = 0; i < sh.c.ncs; ++i) cs = cs || (x0 <= sh.c.csl[i] && sh.c.csl[i] < P);
             cin = (((n1 | l1) >> j) & 1u) || cs ? 1u : 0u;
+            if (JK && !cin && j >= 2u && sh.junk) {
+              // a UTF-8 BOM at a row start right before the run: the row's
+              // first field starts the run (IgnoreUTF8BOM, csv_parser.h:83)
+              const uint8_t *prev = sh.c.text + kPre + (tid - 1) * kSegB;
+              const uint64_t xb = P - 64u + j - 2u;  // the BOM's first byte
+              if (prev[j - 2] == 0xEFu && prev[j - 1] == 0xBBu && prev[j] == 0xBFu) {
+                const uint32_t pb = xb > 0 ? (uint32_t)gbyte(a.text, xb - 1) : (uint32_t)'\n';
+                if (pb == '\n' || pb == '\r' || xb == sh.c.cfloor || t.is_cs(xb)) cin = 1u;
+              }
+            }
           }
         }
       }
@@ -442,23 +452,14 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
         if (JK && sh.junk) {  // block-uniform
           // junk field starts: no value, unless ParseFloat reads one there --
           // the 'f' suffix (the value 0: a token), inf / nan (their values,
-          // inf_nan_of; also after a sign: "-inf" is a number-char token);
-          // "nan(" goes to the exact kernels
+          // inf_nan_of; also after a sign: "-inf" is a number-char token),
+          // "nan(chars)" (NaN; dec_float checks the literal -- round 6: it
+          // no longer sends the input to the exact kernels)
           const uint8_t *seg = sh.c.text + kPre + tid * kSegB;
           auto nv = [&](uint64_t i) { return t.next_cs(P + i) - (P + i); };  // bytes to the chunk end
           for (uint64_t m = F & J; m; m &= m - 1) {
             const uint32_t i = (uint32_t)ctz64(m), k = csv_inf_nan(seg + i, nv(i));
-            if (k == 3u) bad = 1;
-            else if (k != 0u || (seg[i] | 0x20u) == 'f') T |= m & (0 - m);
-          }
-          for (uint64_t m = land & J; m; m &= m - 1)
-            if (csv_inf_nan(seg + ctz64(m), nv(ctz64(m))) == 3u) bad = 1;
-          const uint64_t FD = F & D;
-          uint64_t Jn = J >> 1;  // junk after the byte (a sign's next byte)
-          if (FD >> 63) Jn |= (uint64_t)csv_junk_byte(seg[kSegB]) << 63;
-          for (uint64_t m = FD & Jn; m; m &= m - 1) {
-            const uint32_t i = (uint32_t)ctz64(m), b = seg[i];
-            if ((b == '-' || b == '+') && csv_inf_nan(seg + i + 1, nv(i + 1)) == 3u) bad = 1;
+            if (k != 0u || (seg[i] | 0x20u) == 'f') T |= m & (0 - m);
           }
         }
       } else {
@@ -517,9 +518,11 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
       if constexpr (VT == 0) {
         v = wfloat32m(w4, M, sh.dt, &ok);
         if (junk_tile) {  // inf / nan letters after the optional sign (rare: a branch, not a select)
-          const uint32_t b0 = w4[0] & 0xFFu, l = (b0 == '-' || b0 == '+') ? (w4[0] >> 8) & 0xFFu : b0;
+          const uint32_t b0 = w4[0] & 0xFFu, sg = (b0 == '-' || b0 == '+') ? 1u : 0u, l = (w4[0] >> (8 * sg)) & 0xFFu;
           float x;
           if (((l | 0x20u) == 'i' || (l | 0x20u) == 'n') && inf_nan_of(w4, &x)) v = x;
+          // "nan(chars)": the byte decoder checks the literal (strtonum.h:157-165)
+          if ((l | 0x20u) == 'n' && byte_of(w4, sg + 3u) == '(') ok = false;
         }
       } else {
         v = wint64m(w4, M, &ok);
@@ -531,6 +534,11 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
       if constexpr (VT == 0) {
         bool nan_err = false;
         v = parse_float(src, q, &e, &nan_err);
+        if (MODE == 2 && nan_err) {  // "Invalid NAN literal", at the field's start (csv_core.h csv_line_seq)
+          uint64_t f = q;
+          for (uint32_t b; f > 0 && (b = gbyte(a.text, f - 1)) != a.delim && !is_nl(b) && is_space(b);) --f;
+          raise_error(a.err, E_NAN_LITERAL, f);
+        }
       } else {
         v = c_strtoll(src, q, 0, &e);
       }

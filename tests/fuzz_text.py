@@ -241,8 +241,10 @@ def junk_csv(rng, nlines, maxcols=30, delim=",", header=True, violate=False):
     (csv_parser.h:99-127); an 'f' at a field start is its suffix (the value 0);
     "nan" / "inf" / "Infinity" (any case, after a sign or blanks) are values,
     text after blanks a 0, bytes >= 0x80 junk, and a UTF-8 BOM at a row start
-    is skipped (IgnoreUTF8BOM).  violate=True adds one field the single pass
-    leaves to the exact kernels: ParseFloat's "NaN(...)" form."""
+    is skipped (IgnoreUTF8BOM).  violate=True adds one field of ParseFloat's
+    "NaN(chars)" form (strtonum.h:157-165) -- closed (a NaN), or not (the
+    reference's fatal "Invalid NAN literal") -- which the single pass takes
+    since round 6."""
     ncol = int(rng.integers(1, maxcols + 1))
     out = []
     if header:
@@ -270,7 +272,8 @@ def junk_csv(rng, nlines, maxcols=30, delim=",", header=True, violate=False):
         out.append(bom + row)
     if violate and len(out) > 1:
         k = int(rng.integers(1, len(out)))
-        out[k] = "NaN(1)" + delim + out[k]
+        form = ["NaN(1)", "nan(x_y)", "-nan(ab)", " nan(q)", "NaN(1", "nan(a-b)", "+NAN()"][int(rng.integers(0, 7))]
+        out[k] = form + delim + out[k]
     seps = ["\n"] * 12 + ["\r\n", "\r"]
     text = "".join(line + seps[int(rng.integers(0, len(seps)))] for line in out)
     return text.encode("latin-1")

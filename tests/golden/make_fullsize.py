@@ -61,6 +61,8 @@ CONFIGS = {
     "libsvm_w64_1m_x128": (synth.LIBSVM, po.LIBSVM, 1 << 20, 128, 0),
     # round 6: words and -inf values on every eighth row (svm_fast.h dirty_rewrite)
     "libsvm_dirty_1m_x128": (synth.LIBSVM_DIRTY, po.LIBSVM, 1 << 20, 128, 0),
+    # round 6: a "NaN(x)" field on every 64th row (csv_fast.h: no longer the exact kernels)
+    "csv_dirty_1m_x256": (synth.CSV_NANP, po.CSV, 1 << 20, 256, 0),
 }
 for _r in range(8):  # config 5: bench.py's rank r shard of 32M x 64 (4M rows from row r * 4M)
     CONFIGS["libsvm_32m_x64_part%d" % _r] = (synth.LIBSVM, po.LIBSVM, 4 << 20, 64, _r * (4 << 20))

@@ -553,9 +553,9 @@ def test_emu_csv_fast_text_fields():
     csv_junk_byte): header rows, text columns, words and numbers followed by
     text -- a field starting with text holds no value, text after a number
     ends it; "nan" / "inf" / "f" fields are values (also after a sign or
-    blanks), text after blanks a 0, a BOM at a row start skipped; "NaN(...)"
-    goes to the exact kernels.  Multi-tile, odd chunkings, both ',' and ' '
-    delimiters."""
+    blanks), text after blanks a 0, a BOM at a row start skipped, "NaN(...)"
+    a NaN or the reference's literal error (round 6: no longer the exact
+    kernels).  Multi-tile, odd chunkings, both ',' and ' ' delimiters."""
     rng = np.random.default_rng(77)
     paths = {"fast": 0, "exact": 0}
     for it in range(40):
@@ -573,11 +573,9 @@ def test_emu_csv_fast_text_fields():
         if not failed:
             assert diff(h, o) == [], (it, diff(h, o), data[:300])
         paths[h["path"]] += 1
-        if not violate and delim == ",":
+        if delim == ",":
             assert h["path"] == "fast", (it, data[:300])
-        if violate:
-            assert h["path"] == "exact" or failed, (it, data[:300])
-    assert paths["fast"] >= 20 and paths["exact"] >= 4, paths
+    assert paths["fast"] >= 20, paths
 
 
 @pytest.mark.parametrize("vt", [0, 1, 2])

@@ -534,8 +534,9 @@ def test_gpu_csv_fast_text_fields_vs_oracle(dm):
     """Text in CSV float columns on the single-pass kernel (csv_fast.h
     csv_junk_byte): header rows, text columns, numbers followed by text,
     "nan" / "inf" / "f" fields (after signs and blanks too), bytes >= 0x80 and
-    BOMs at row starts stay on it; "NaN(...)" takes the exact kernels.  Either
-    path gives the reference's result."""
+    BOMs at row starts stay on it, and so (round 6) do "NaN(...)" fields --
+    closed, or not (the reference's "Invalid NAN literal").  Either path gives
+    the reference's result."""
     rng = np.random.default_rng(4711)
     paths = {"fast": 0, "exact": 0}
     for it in range(160):
@@ -550,11 +551,9 @@ def test_gpu_csv_fast_text_fields_vs_oracle(dm):
         except AssertionError as e:
             raise AssertionError("case %d: %s" % (it, e))
         paths[h["path"]] += 1
-        if not violate and delim == ",":
+        if delim == ",":
             assert h["path"] == "fast", (it, data[:200])
-        if violate:
-            assert h["path"] == "exact" or h["failed"], (it, data[:200])
-    assert paths["fast"] > 80 and paths["exact"] > 10, paths
+    assert paths["fast"] > 80, paths
 
 
 def test_gpu_csv_header_row_bench_shape(dm):

@@ -31,6 +31,9 @@
  *    infinite value "<id>:-inf" -- bytes outside the uniform grammar that
  *    ParsePair skips (strtonum.h:667-703) and ParseFloat's inf
  *    (strtonum.h:133-175).
+ *  CSV with NaN(chars) fields (fmt 10): the CSV row, and on every 64th row
+ *    (r % 64 == 17) the middle field "NaN(x)" -- ParseFloat's NAN(chars)
+ *    form (strtonum.h:157-165), a quiet NaN.
  *  CSV with missing values (fmt 7): the CSV row with 0.1 % of its fields
  *    "nan" (numpy.savetxt's missing value; ParseFloat's NAN branch,
  *    strtonum.h:133-175), and a UTF-8 BOM at the head of the file
@@ -96,13 +99,14 @@ static size_t fmt_libfm_row(char *o, uint64_t seed, uint64_t r, int K) {
   return (size_t)(p - o);
 }
 
-static size_t fmt_csv_row(char *o, uint64_t seed, uint64_t r, int C, int blank, int nan) {
+static size_t fmt_csv_row(char *o, uint64_t seed, uint64_t r, int C, int blank, int nan, int nanp) {
   uint64_t s = row_state(seed, r);
   char *p = o;
   for (int j = 0; j < C; ++j) {
     uint64_t x = sm64(&s);
     float v = (float)(x >> 40) * (1.0f / 8388608.0f) - 1.0f;
     if (nan && ((x >> 8) & 0xFFFF) % 1000 == 0) p += sprintf(p, j ? ",nan" : "nan");
+    else if (nanp && (r & 63) == 17 && j == C / 2) p += sprintf(p, j ? ",NaN(x)" : "NaN(x)");
     else p += sprintf(p, j ? (blank ? ", %.9g" : ",%.9g") : "%.9g", (double)v);
   }
   *p++ = '\n';
@@ -140,7 +144,7 @@ size_t synth_rows(int fmt, uint64_t row0, uint64_t nrows, int width, uint64_t se
       n += fmt == 0 || fmt == 3 || fmt == 4 || fmt == 6 || fmt == 8 || fmt == 9
                ? fmt_libsvm_row(buf + n, seed, row0 + r, width, fmt == 3, fmt == 4, fmt == 6, fmt == 9)
                     : fmt == 2 ? fmt_libfm_row(buf + n, seed, row0 + r, width)
-                               : fmt_csv_row(buf + n, seed, row0 + r, width, fmt == 5, fmt == 7);
+                               : fmt_csv_row(buf + n, seed, row0 + r, width, fmt == 5, fmt == 7, fmt == 10);
     }
     bbuf[b] = buf;
     bsz[b] = n;

@@ -7,7 +7,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB = None
 
-LIBSVM, CSV, LIBFM, LIBSVM_QID, LIBSVM_CMT, CSV_SP, LIBSVM_1B, CSV_NAN, LIBSVM_HDRS, LIBSVM_DIRTY = 0, 1, 2, 3, 4, 5, 6, 7, 8, 9
+LIBSVM, CSV, LIBFM, LIBSVM_QID, LIBSVM_CMT, CSV_SP, LIBSVM_1B, CSV_NAN, LIBSVM_HDRS, LIBSVM_DIRTY, CSV_NANP = 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10
 
 
 def lib():

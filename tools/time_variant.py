@@ -19,6 +19,7 @@ fmt, rows, width, kind = {"libsvm": ("libsvm", 1 << 20, 128, synth.LIBSVM), "csv
                           "cmt": ("libsvm", 1 << 20, 128, synth.LIBSVM_CMT),
                           "hdrs": ("libsvm", 1 << 20, 128, synth.LIBSVM_HDRS),
                           "dirty": ("libsvm", 1 << 20, 128, synth.LIBSVM_DIRTY),
+                          "csv_dirty": ("csv", 1 << 20, 256, synth.CSV_NANP),
                           "libfm": ("libfm", 1 << 20, 64, synth.LIBFM),
                           "csv_nan": ("csv", 1 << 20, 256, synth.CSV_NAN),
                           "exact": ("libsvm", 1 << 20, 128, synth.LIBSVM),
