@@ -1361,6 +1361,7 @@ DA_HDF uint32_t dirty_lines(const Tile &t, Shared &sh, uint32_t bad, BK &bk, At 
 // before its pre-halo declines.  Returns the tile's flags as dirty_lines;
 // *took: false when the tile declined (block-uniform).
 constexpr uint32_t kDeclined = 1u << 16;  // Shared::hashy: dirty_rewrite declined the tile
+constexpr uint32_t kOutside = 1u << 17;   // Shared::hashy: bytes outside the grammar left after the comment pass
 template <class BK, class At>
 DA_HDF uint32_t dirty_rewrite(const Tile &t, Shared &sh, uint32_t bad, BK &bk, At at, uint32_t k, bool *took) {
   (void)k;
@@ -1369,6 +1370,14 @@ DA_HDF uint32_t dirty_rewrite(const Tile &t, Shared &sh, uint32_t bad, BK &bk, A
   const uint64_t n = t.a->n;
   const uint64_t P = t.tlo + (uint64_t)tid * kSegB;
   const bool pre = t.tlo > 0;  // slot 0 holds the 64 bytes before the tile
+  // nothing outside the grammar left (the comment pass took it all): done
+  if ((P < n && outside_mask(t, sh, tid) != 0) || (tid == 0 && pre && sh.prebad != 0))
+    atomic_or_u32(&sh.hashy, kOutside);
+  bk.sync();
+  if (!(sh.hashy & kOutside)) {  // block-uniform
+    *took = true;
+    return bad;
+  }
   // outside bytes of slot s (0: the pre-halo)
   auto x_of = [&](int s) -> uint64_t { return s == 0 ? (pre ? sh.prebad : 0ull) : outside_mask(t, sh, s - 1); };
   // the gap state after slot s: 1 when its last non-blank byte is a

@@ -478,7 +478,7 @@ def dirty_libsvm(rng, nbytes, rate=0.002, long_frac=0.0, near_tile_end=False, eo
 # nan forms after a sign (strtonum.h:133-175).  (An unsigned "nan" value
 # is skipped to the next run, "a:b:c" -- the exact kernels take that.)
 ROW_TOKENS = [b"NA", b"null", b"did", b"x", b"~", b"@@", b"qi", b"dq", b"x#y", b"\x0b", b"\xc3\xa9t\xc3\xa9", b"!",
-              b"n/a", b"q:", b"::"]
+              b"n/a", b"q:"]
 # tokens holding digitchar runs of their own (read as index-only ids: a block
 # mixing them with valued pairs fails the reference's RowBlock CHECK,
 # row_block.h:178 -- the tests then compare the failure)
