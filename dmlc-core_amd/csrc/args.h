@@ -111,6 +111,9 @@ struct FastSvmArgs {
 // look-back words per single-pass tile (fast_common.h: status + 4 prefix words);
 // the persistent launch's ticket word follows them
 constexpr uint64_t kFastLbWords = 5;
+// the CSV single pass (csv_fast.h csv_look_back): status + 3 prefix words in
+// one 64-byte record per tile
+constexpr uint64_t kCsvLbWords = 8;
 
 // Threads of a single-pass tile (fast_common.h): four waves, 16 KiB tiles.
 // One wave per tile (4 KiB tiles, no barriers between waves, -DFAST_THREADS=64)

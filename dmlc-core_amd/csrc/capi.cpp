@@ -147,8 +147,10 @@ uint64_t rec_bytes_of(uint64_t nbytes, uint64_t T, uint64_t ntiles, const dmlc_a
 }
 
 // single-pass look-back words: the full kernel's [5 nft] + its ticket; libsvm
-// adds the lean kernel's [5 nft] + its poison word (libsvm.hip)
+// adds the lean kernel's [5 nft] + its poison word (libsvm.hip); CSV keeps
+// one 8-word record per tile (csv_fast.h csv_look_back)
 uint64_t lb_words_of(uint64_t nft, const dmlc_amd_params *prm) {
+  if (prm && prm->format == DMLC_AMD_CSV) return nft * dmlc_amd::kCsvLbWords + 1;
   return prm && prm->format == DMLC_AMD_LIBSVM ? nft * 10 + 2 : nft * 5 + 1;
 }
 

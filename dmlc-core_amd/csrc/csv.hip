@@ -91,7 +91,7 @@ hipError_t launch_csv(const CsvArgs &a, const FastCsvArgs &f, bool use_fast, uin
   fl.add(reinterpret_cast<uint64_t *>(f.err), 1, ~0ull);
   const bool sp = f.label_col >= 0 || f.weight_col >= 0;
   if (use_fast) {
-    fl.add(f.lb, (uint64_t)f.ntiles * 8, 0);
+    fl.add(f.lb, (uint64_t)f.ntiles * kCsvLbWords, 0);
     if (sp) fl.add(f.labsum, kLabShards * 8, 0);
   }
   if (!a.ntiles && phase != kPhaseCount) fl.add(reinterpret_cast<uint64_t *>(a.offset), 1, 0);  // empty input: offset = {0}

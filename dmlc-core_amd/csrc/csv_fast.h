@@ -164,7 +164,7 @@ DA_HDF uint32_t csv_look_back(uint64_t *lb, uint32_t k, const uint32_t cnt[4], u
     // tile 0: an inclusive 0); the prefix stands when all three carry kMark
     uint64_t s = 0, w[3] = {kMark, kMark, kMark};
     if (lane < j) {
-      const uint64_t *rec = lb + (j - 1 - lane) * 8;
+      const uint64_t *rec = lb + (j - 1 - lane) * kCsvLbWords;
       s = load_agent_u64(const_cast<uint64_t *>(rec));
 #pragma unroll
       for (int i = 0; i < 3; ++i) w[i] = load_agent_u64(const_cast<uint64_t *>(rec) + 1 + i);
@@ -204,7 +204,7 @@ DA_HDF uint32_t csv_look_back(uint64_t *lb, uint32_t k, const uint32_t cnt[4], u
     c.base[Q_VALS] = vals;
     *segc = tail;
   }
-  uint64_t *rec = lb + (uint64_t)k * 8;
+  uint64_t *rec = lb + (uint64_t)k * kCsvLbWords;
   if (lane < 3) {
     const uint64_t v = lane == 0 ? rows + cnt[0] : lane == 1 ? vals + cnt[1]
                                                            : (cnt[3] ? (uint64_t)cnt[2] : tail + cnt[2]);
@@ -490,7 +490,7 @@ DA_HDF void tile(const FastCsvArgs &a, Shared &sh, BK &bk, uint32_t k) {
   const uint32_t nR = (uint32_t)(totp & 0xFFFF), nT = (uint32_t)((totp >> 16) & 0xFFFF);
   const uint32_t cnt4[4] = {nR, nT, (uint32_t)((totp >> 32) & 0x7FFFFFFF), (uint32_t)(totp >> 63)};
   if (tid == 0) {
-    uint64_t *rec = a.lb + (uint64_t)k * 8;
+    uint64_t *rec = a.lb + (uint64_t)k * kCsvLbWords;
     const uint64_t packed = (uint64_t)cnt4[0] | ((uint64_t)cnt4[1] << 15) | ((uint64_t)cnt4[2] << 30) |
                             ((uint64_t)cnt4[3] << 45);
     if (k == 0) {

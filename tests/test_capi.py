@@ -72,6 +72,16 @@ def test_workspace_and_argument_validation(lib):
             extra = (dmlc_amd.lib().dmlc_amd_workspace_bytes(n, 128, ctypes.byref(q))
                      - dmlc_amd.lib().dmlc_amd_workspace_bytes(n, 128, ctypes.byref(base)))
             assert extra <= n // 8 * 5 + (1 << 20) + 4096, (tb, n, extra)
+    # the CSV single pass keeps an 8-word look-back record per 16 KiB tile (args.h kCsvLbWords),
+    # libfm 5 (kFastLbWords): with the exact kernels' records off (64-byte exact tiles) the
+    # difference is those words alone -- round 6 sized CSV at 5 and its records ran into labsum
+    n = 1 << 30
+    nft = n // tile
+    c64 = dmlc_amd.make_params("csv", tile_bytes=64)
+    f64 = dmlc_amd.make_params("libfm", tile_bytes=64)
+    d = (dmlc_amd.lib().dmlc_amd_workspace_bytes(n, 128, ctypes.byref(c64))
+         - dmlc_amd.lib().dmlc_amd_workspace_bytes(n, 128, ctypes.byref(f64)))
+    assert d == nft * 3 * 8, (d, nft)
     # bad index_bits is rejected before any device work
     bad = dmlc_amd.make_params("libsvm", index_bits=16)
     csr = dmlc_amd.Csr()
