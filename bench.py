@@ -373,10 +373,15 @@ def main():
     dom_bytes = nbytes + b_out
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
     traffic = None
+    build = dmlc_amd.build_id()
+    traffic_src = None
     try:  # HBM bytes per launch measured by rocprofv3 PMC passes (tools/gpu_pmc.sh) on this kernel
         tr = json.load(open(os.path.join(ROOT, "profiles", "traffic.json"))).get(args.config)
         if tr and tr["kernel"] == kern_name and not args.rows and not args.tile_bytes:
             traffic = tr["hbm_bytes_per_launch"]
+            # which build the PMC passes ran on (tools/traffic_update.py), and whether it is this one
+            traffic_src = {"build": tr.get("build"), "same_build": tr.get("build") == build,
+                           "source": tr.get("source")}
     except (OSError, ValueError):
         pass
     par = "shard%d" % world
@@ -409,7 +414,9 @@ def main():
         "roofline": {"bound": "hbm", "kernel": kern_name, "achieved": round(achieved, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "bytes_per_launch": dom_bytes, "avg_ms": round(dom_ms, 4)},
+                     "bytes_per_launch": dom_bytes, "avg_ms": round(dom_ms, 4),
+                     "traffic_measured_on": traffic_src},
+        "build": build,
         "cpu_baseline": None,
     }
     if world > 1:

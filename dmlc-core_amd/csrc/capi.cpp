@@ -109,6 +109,11 @@ int dmlc_amd_profile_end(double *total_ms, int *launches, const char **kernel) {
 
 int dmlc_amd_abi_version(void) { return DMLC_AMD_ABI_VERSION; }
 
+#ifndef DMLC_AMD_BUILD_ID
+#define DMLC_AMD_BUILD_ID "unknown"
+#endif
+const char *dmlc_amd_build_id(void) { return DMLC_AMD_BUILD_ID; }
+
 int dmlc_amd_fast_geometry(uint32_t *tile_bytes, uint32_t *max_unit_starts) {
   if (tile_bytes) *tile_bytes = (uint32_t)dmlc_amd::kFastTileBytes;
   if (max_unit_starts) *max_unit_starts = (uint32_t)dmlc_amd::kFastMaxCs;

@@ -67,6 +67,7 @@ def lib():
         L.dmlc_amd_error_string.argtypes = [ctypes.c_int]
         L.dmlc_amd_device_count.restype = ctypes.c_int
         L.dmlc_amd_abi_version.restype = ctypes.c_int
+        L.dmlc_amd_build_id.restype = ctypes.c_char_p
         L.dmlc_amd_strtof_batch.restype = ctypes.c_int
         L.dmlc_amd_strtof_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
@@ -104,7 +105,8 @@ def profile_end():
 EXPORTED_SYMBOLS = ("dmlc_amd_parse", "dmlc_amd_workspace_bytes", "dmlc_amd_error_string",
                     "dmlc_amd_device_count", "dmlc_amd_abi_version", "dmlc_amd_strtof_batch",
                     "dmlc_amd_profile_begin", "dmlc_amd_profile_end", "dmlc_amd_last_hip_error",
-                    "dmlc_amd_copy", "dmlc_amd_copy_n", "dmlc_amd_copy_n_dev", "dmlc_amd_fast_geometry")
+                    "dmlc_amd_copy", "dmlc_amd_copy_n", "dmlc_amd_copy_n_dev", "dmlc_amd_fast_geometry",
+                    "dmlc_amd_build_id")
 
 
 def fast_geometry():
@@ -256,6 +258,11 @@ class DeviceParser:
         out["result_counts"] = [int(x) for x in r[:8]]
         out["max_index"], out["max_field"] = int(r[10]), int(r[11])
         return out
+
+
+def build_id():
+    """SHA-256 prefix of the sources the loaded library was built from."""
+    return lib().dmlc_amd_build_id().decode()
 
 
 def error_code(err):

@@ -186,6 +186,12 @@ int dmlc_amd_device_count(void);
 /* ABI version this library was built with. */
 int dmlc_amd_abi_version(void);
 
+/* Build id: SHA-256 (first 16 hex digits) of the kernel and C-ABI sources
+ * this library was compiled from (dmlc-core_amd/Makefile).  bench.py stamps
+ * its line with it and with the build id of the PMC run its HBM traffic
+ * figure came from (profiles/traffic.json).  Not a reference interface. */
+const char *dmlc_amd_build_id(void);
+
 /* Geometry of the single-pass kernels this library was built with: text
  * bytes per tile and the most ParseBlock unit starts one tile takes before
  * the call goes to the exact kernels (diagnostics and tests; either pointer
