@@ -65,6 +65,7 @@ CONFIGS = {
     # mixes) on configs 2 / 3, forced with DMLC_AMD_FLAG_EXACT
     "libsvm_exact_1m_x128": ("libsvm", 1 << 20, 128, None),
     "csv_exact_1m_x256": ("csv", 1 << 20, 256, None),
+    "libfm_exact_1m_x64": ("libfm", 1 << 20, 64, None),
 }
 # parser arguments per config (dmlc_amd_params; the reference's URI args)
 PARAMS = {
@@ -74,6 +75,7 @@ PARAMS = {
     "csv_i32_1m_x256": {"value_type": "i32"},
     "libsvm_exact_1m_x128": {"flags": dmlc_amd.FLAG_EXACT},
     "csv_exact_1m_x256": {"flags": dmlc_amd.FLAG_EXACT},
+    "libfm_exact_1m_x64": {"flags": dmlc_amd.FLAG_EXACT},
 }
 DESC = {
     "libsvm_1m_x128": "libsvm 1M rows x 128 nnz/row, device-resident",
@@ -95,6 +97,7 @@ DESC = {
     "csv_dirty_1m_x256": "CSV dense 1M rows x 256 float cols, every 64th row's middle field \"NaN(x)\" (ParseFloat's NAN(chars) form), device-resident",
     "libsvm_exact_1m_x128": "libsvm 1M rows x 128 nnz/row on the exact kernels (DMLC_AMD_FLAG_EXACT), device-resident",
     "csv_exact_1m_x256": "CSV dense 1M rows x 256 float cols on the exact kernels (DMLC_AMD_FLAG_EXACT), device-resident",
+    "libfm_exact_1m_x64": "libfm 1M rows x 64 field:id:value/row on the exact kernels (DMLC_AMD_FLAG_EXACT), device-resident",
 }
 SYNTH = {"libsvm": synth.LIBSVM, "csv": synth.CSV, "libfm": synth.LIBFM, "libsvm_qid": synth.LIBSVM_QID,
          "libsvm_cmt": synth.LIBSVM_CMT, "csv_sp": synth.CSV_SP, "libsvm_1b": synth.LIBSVM_1B,

@@ -8,7 +8,8 @@
 // the line starts in their byte range, 8 KiB LDS windows, the owner of a line
 // start parses its head and marks R1, the first feature run).  The feature
 // runs of a line then follow ParseTriple's grammar as a 4-state machine whose
-// per-segment transition functions compose in a block scan:
+// per-segment transition functions compose in a block scan; one walk per
+// segment records the role masks for every start state (walk_roles):
 //
 //   state  meaning (the role of the last run)      next run, gap's first non-blank
 //   PRE    head / nothing yet                        -> PRE (no role until R1)
@@ -83,141 +84,204 @@ DA_HD uint64_t prev_run(const F &at, uint64_t x, uint64_t floor) {
   return x;
 }
 
-// Event walk over one segment.  MODE 0: compose the transition function into
-// st; MODE 1: count from concrete state st; MODE 2: count and emit.
-template <int MODE>
-DA_HDF void walk(const LibfmArgs &a, Src &src, const uint32_t *r1bits, uint64_t w0, const Seg &sg,
-                 uint32_t &st, Cnt &cnt, const Base64 &base, MinAcc *macc = nullptr,
-                 const fast::DecTables *dt = nullptr) {
+// Role masks of one segment for each state at its start (libsvm_core.h
+// Roles, with ParseTriple's four states): bit i of pr[s] / va[s] = the run
+// at lo + i is the index of a (field, index) pair / a value when the segment
+// starts in state s; dp[s] / dv[s] = a dangling "v1:" / "v1:v2:" at the line
+// end at lo + i, whose index / value ParseTriple decodes at lo + i + 1; neg:
+// per state (byte s) the first run read as v1 that starts with '-' (0xFF:
+// none) -- the reference decodes every v1, so it raises the sign error even
+// when the triple is dropped (strtonum.h:416).  The block scan of the
+// transition functions picks one set; counts are popcounts.  Round 6: one
+// walk per window instead of three (compose, count, emit).
+struct Roles {
+  uint32_t pr[4], va[4], dp[4], dv[4];
+  uint32_t neg;
+};
+DA_HD uint32_t pick(const uint32_t m[4], uint32_t s) {  // m[s] without a dynamic register index
+  return s == 0 ? m[0] : s == 1 ? m[1] : s == 2 ? m[2] : m[3];
+}
+
+// Event walk over one segment: the transition function (4 x 2-bit entries,
+// entry s = the state after the events when the segment starts in s) and
+// the role masks.  ParseTriple (strtonum.h:718-772) for libfm_parser.h:
+// 100-139: after the head (R1) runs are v1 / v2 / v3 by the ':' between them.
+DA_HDF void walk_roles(const LibfmArgs &a, Src &src, const uint32_t *r1bits, uint64_t w0, const Seg &sg,
+                       uint32_t &fn, Roles &R) {
+  for (int s = 0; s < 4; ++s) R.pr[s] = R.va[s] = R.dp[s] = R.dv[s] = 0;
+  R.neg = ~0u;
   uint32_t ev = sg.rs | sg.ls | sg.le;
   int chunk = sg.chunk;
   uint64_t cfloor = a.cs[chunk], cend = a.cs[chunk + 1];
   src.lim = a.lim(chunk);  // decoders read to the InputSplit chunk end
-  // one (field, index) pair: decode, check signs, store / track the chunk minimum
-  auto pair = [&](uint64_t fpos, uint64_t ipos, uint64_t x) {
-    if (MODE == 2 || macc) {
-      uint64_t fv, iv;
-      bool ok = index_at(src, fpos, a.wide != 0, dt, &fv);  // (exact_dec.h)
-      ok = index_at(src, ipos, a.wide != 0, dt, &iv) && ok;
-      if (!ok) {
-        raise_error(a.err, E_NEG_INDEX, x);
-        fv = iv = 0;
-      }
-      if (MODE == 1) {
-        if (!a.wide) {
-          fv = (uint32_t)fv;
-          iv = (uint32_t)iv;
-        }
-        macc->add(a.chunk_min, chunk, fv < iv ? fv : iv);
-      } else {
-        if (a.indexing_mode > 0 || (a.indexing_mode < 0 && a.chunk_min[chunk] > 0)) {
-          --fv;
-          --iv;
-        }
-        const uint64_t r = base.c[C_INDEX] + cnt.c[C_INDEX];
-        if (r < a.cap[C_INDEX] && r < a.cap[C_FIELD]) {
-          if (a.wide) {
-            reinterpret_cast<uint64_t *>(a.index)[r] = iv;
-            reinterpret_cast<uint64_t *>(a.field)[r] = fv;
-          } else {
-            reinterpret_cast<uint32_t *>(a.index)[r] = (uint32_t)iv;
-            reinterpret_cast<uint32_t *>(a.field)[r] = (uint32_t)fv;
-          }
-        } else {
-          raise_error(a.err, E_CAPACITY, x);
-        }
-      }
-    }
-    cnt.c[C_INDEX]++;
-    cnt.c[C_FIELD]++;
-  };
-  auto value = [&](uint64_t vpos, uint64_t x) {
-    if (MODE == 2) {
-      const uint64_t r = base.c[C_VALUE] + cnt.c[C_VALUE];
-      bool nan_err = false;
-      const float v = value_at(src, vpos, dt, &nan_err);
-      if (nan_err) raise_error(a.err, E_NAN_LITERAL, x);
-      if (r < a.cap[C_VALUE]) a.value[r] = v;
-      else raise_error(a.err, E_CAPACITY, x);
-    }
-    cnt.c[C_VALUE]++;
-  };
   while (ev) {
     const int i = ctz32(ev);
     ev &= ev - 1;
+    const uint32_t bit = 1u << i;
     const uint64_t x = sg.lo + i;
     while (x >= cend) {  // entered the next chunk
       ++chunk;
       cfloor = a.cs[chunk];
       cend = a.cs[chunk + 1];
-      src.lim = a.lim(chunk);  // decoders read to the InputSplit chunk end
+      src.lim = a.lim(chunk);
     }
-    if ((sg.ls >> i) & 1u) {
-      if (MODE == 0) {
-        st = kAllPre;
-      } else {
-        st = S_PRE;
-        const bool l0 = x == cfloor;
-        const Head h = head_parse(src, x, cend);
-        if (MODE == 2 && l0) {
-          uint64_t *row = a.chunk_tab + (uint64_t)chunk * 8;  // rows of 8 slots (dmlc_amd.h)
-          for (int k = 0; k < C_N; ++k) row[k] = base.c[k] + cnt.c[k];
+    if (sg.ls & bit) fn = kAllPre;
+    if (sg.rs & bit) {
+      uint32_t amask = 0;  // states in which the run is a v1
+      if (r1_bit(r1bits, w0, x)) {
+        fn = kAllA;
+        amask = 0xFu;
+      } else if (fn != kAllPre) {
+        const bool colon = gap_fnb(src, x, cfloor) == ':';
+        for (int s = 0; s < 4; ++s) {
+          const uint32_t e = (fn >> (2 * s)) & 3u;
+          if (e == S_A && colon) R.pr[s] |= bit;
+          else if (e == S_B && colon) R.va[s] |= bit;
+          else if (e != S_PRE) amask |= 1u << s;
         }
-        if (h.row) {
-          if (MODE == 2) {
-            const uint64_t r = base.c[C_ROWS] + cnt.c[C_ROWS];
-            bool nan_err = false;
-            uint64_t e;
-            if (r < a.cap[C_ROWS]) {
-              a.label[r] = parse_float(src, h.label, &e, &nan_err);
-              a.offset[r] = base.c[C_INDEX] + cnt.c[C_INDEX];
-            } else {
-              raise_error(a.err, E_CAPACITY, x);
-            }
-            if (h.w) {
-              const uint64_t wr = base.c[C_WEIGHT] + cnt.c[C_WEIGHT];
-              if (wr < a.cap[C_WEIGHT]) a.weight[wr] = parse_float(src, h.wpos, &e, &nan_err);
-              else raise_error(a.err, E_CAPACITY, x);
-            }
-            if (nan_err) raise_error(a.err, E_NAN_LITERAL, x);
-          }
-          cnt.c[C_ROWS]++;
-          cnt.c[C_LABEL]++;
-          cnt.c[C_WEIGHT] += h.w;
-        }
+        fn = fn_apply(fn, colon ? kTColon : kTOther);
       }
+      if (amask && src(x) == '-')
+        for (int s = 0; s < 4; ++s)
+          if (((amask >> s) & 1u) && ((R.neg >> (8 * s)) & 0xFFu) == 0xFFu)
+            R.neg = (R.neg & ~(0xFFu << (8 * s))) | ((uint32_t)i << (8 * s));
     }
-    if ((sg.rs >> i) & 1u) {
-      if (MODE == 0) {
-        if (r1_bit(r1bits, w0, x)) {
-          st = kAllA;
-        } else if (st != kAllPre) {
-          st = fn_apply(st, gap_fnb(src, x, cfloor) == ':' ? kTColon : kTOther);
-        }
-      } else {
-        uint32_t role = S_PRE;
-        if (r1_bit(r1bits, w0, x)) {
-          role = S_A;
-        } else if (st != S_PRE) {
-          const bool colon = gap_fnb(src, x, cfloor) == ':';
-          role = (st == S_A && colon) ? S_B : (st == S_B && colon) ? S_C : S_A;
-        }
-        if (role != S_PRE) st = role;
-        if (role == S_A) {  // v1 of a triple: the reference decodes it even if dropped
-          // (ParseUnsignedInt fails only on a leading '-': x starts a digitchar run)
-          if (MODE == 2 && src(x) == '-') raise_error(a.err, E_NEG_INDEX, x);
-        } else if (role == S_B) {
-          pair(prev_run(src, x, cfloor), x, x);
-        } else if (role == S_C) {
-          value(x, x);
-        }
+    if (sg.le & bit) {  // "v1:" / "v1:v2:" at the line end: ParseTriple decodes at lend
+      uint32_t fA = 0, fB = 0;
+      for (int s = 0; s < 4; ++s) {
+        const uint32_t e = (fn >> (2 * s)) & 3u;
+        fA |= (e == S_A ? 1u : 0u) << s;
+        fB |= (e == S_B ? 1u : 0u) << s;
       }
+      if ((fA | fB) && gap_fnb(src, x + 1, cfloor) == ':')
+        for (int s = 0; s < 4; ++s) {
+          if ((fA >> s) & 1u) R.dp[s] |= bit;
+          if ((fB >> s) & 1u) R.dv[s] |= bit;
+        }
     }
-    if (MODE != 0 && ((sg.le >> i) & 1u) && (st == S_A || st == S_B)) {
-      // "v1:" / "v1:v2:" at the line end: ParseTriple decodes at lend
-      if (gap_fnb(src, x + 1, cfloor) == ':') {
-        if (st == S_A) pair(prev_run(src, x + 1, cfloor), x + 1, x);
-        else value(x + 1, x);
+  }
+}
+
+DA_HD int chunk_at(const LibfmArgs &a, int chunk, uint64_t x) {
+  while (x >= a.cs[chunk + 1]) ++chunk;
+  return chunk;
+}
+
+// The (field, index) pairs of the segment in position order (P: pairs at run
+// starts, D: dangling pairs at line ends, index at lo + i + 1): f(rank, field
+// value, index value, event position, chunk); the sign error is raised here.
+template <typename F>
+DA_HDF void for_pairs(const LibfmArgs &a, Src &src, const Seg &sg, uint32_t P, uint32_t D,
+                      const fast::DecTables *dt, F &&f) {
+  int chunk = sg.chunk;
+  uint64_t cfloor = a.cs[chunk];
+  src.lim = a.lim(chunk);
+  uint64_t r = 0;
+  for (uint32_t m = P | D; m; m &= m - 1, ++r) {
+    const uint32_t i = (uint32_t)ctz32(m);
+    const uint64_t x = sg.lo + i;
+    if (x >= a.cs[chunk + 1]) {
+      chunk = chunk_at(a, chunk, x);
+      cfloor = a.cs[chunk];
+      src.lim = a.lim(chunk);
+    }
+    const uint64_t ip = x + ((D >> i) & 1u);
+    uint64_t fv, iv;
+    bool ok = index_at(src, prev_run(src, ip, cfloor), a.wide != 0, dt, &fv);  // (exact_dec.h)
+    ok = index_at(src, ip, a.wide != 0, dt, &iv) && ok;
+    if (!ok) {
+      raise_error(a.err, E_NEG_INDEX, x);
+      fv = iv = 0;
+    }
+    f(r, fv, iv, x, chunk);
+  }
+}
+
+// Write pass: the segment's pairs, values and rows at base + their rank in
+// the segment (masks of its start state; libsvm_core.h emit).
+DA_HDF void emit(const LibfmArgs &a, Src &src, const Seg &sg, uint32_t P, uint32_t V, uint32_t DP, uint32_t DV,
+                 uint32_t neg, const Base64 &base, const fast::DecTables *dt) {
+  if (neg != 0xFFu) raise_error(a.err, E_NEG_INDEX, sg.lo + neg);
+  // ---- (field, index) pairs
+  for_pairs(a, src, sg, P, DP, dt, [&](uint64_t rk, uint64_t fv, uint64_t iv, uint64_t x, int chunk) {
+    if (a.indexing_mode > 0 || (a.indexing_mode < 0 && a.chunk_min[chunk] > 0)) {
+      --fv;
+      --iv;
+    }
+    const uint64_t r = base.c[C_INDEX] + rk;
+    if (r < a.cap[C_INDEX] && r < a.cap[C_FIELD]) {
+      if (a.wide) {
+        reinterpret_cast<uint64_t *>(a.index)[r] = iv;
+        reinterpret_cast<uint64_t *>(a.field)[r] = fv;
+      } else {
+        reinterpret_cast<uint32_t *>(a.index)[r] = (uint32_t)iv;
+        reinterpret_cast<uint32_t *>(a.field)[r] = (uint32_t)fv;
+      }
+    } else {
+      raise_error(a.err, E_CAPACITY, x);
+    }
+  });
+  // ---- values (a v3 run, or the value read at the line end after "v1:v2:")
+  {
+    int chunk = sg.chunk;
+    src.lim = a.lim(chunk);
+    uint64_t vr = base.c[C_VALUE];
+    for (uint32_t m = V | DV; m; m &= m - 1, ++vr) {
+      const uint32_t i = (uint32_t)ctz32(m);
+      const uint64_t x = sg.lo + i;
+      if (x >= a.cs[chunk + 1]) {
+        chunk = chunk_at(a, chunk, x);
+        src.lim = a.lim(chunk);
+      }
+      bool nan_err = false;
+      const float v = value_at(src, x + ((DV >> i) & 1u), dt, &nan_err);
+      if (nan_err) raise_error(a.err, E_NAN_LITERAL, x);
+      if (vr < a.cap[C_VALUE]) a.value[vr] = v;
+      else raise_error(a.err, E_CAPACITY, x);
+    }
+  }
+  // ---- rows: label[:weight] heads, row offsets, unit table rows
+  if (sg.ls) {
+    Cnt cnt = cnt_zero();  // rows / labels / weights so far in the segment
+    int chunk = sg.chunk;
+    uint64_t cfloor = a.cs[chunk], cend = a.cs[chunk + 1];
+    src.lim = a.lim(chunk);
+    for (uint32_t m = sg.ls; m; m &= m - 1) {
+      const uint32_t i = (uint32_t)ctz32(m);
+      const uint64_t x = sg.lo + i;
+      while (x >= cend) {
+        ++chunk;
+        cfloor = a.cs[chunk];
+        cend = a.cs[chunk + 1];
+        src.lim = a.lim(chunk);
+      }
+      const uint32_t below = (1u << i) - 1u;
+      cnt.c[C_INDEX] = cnt.c[C_FIELD] = (uint32_t)popc32((P | DP) & below);
+      cnt.c[C_VALUE] = (uint32_t)popc32((V | DV) & below);
+      if (x == cfloor) {
+        uint64_t *row = a.chunk_tab + (uint64_t)chunk * 8;  // rows of 8 slots (dmlc_amd.h)
+        for (int k = 0; k < C_N; ++k) row[k] = base.c[k] + cnt.c[k];
+      }
+      const Head h = head_parse(src, x, cend);
+      if (h.row) {
+        const uint64_t r = base.c[C_ROWS] + cnt.c[C_ROWS];
+        bool nan_err = false;
+        uint64_t e;
+        if (r < a.cap[C_ROWS]) {
+          a.label[r] = parse_float(src, h.label, &e, &nan_err);
+          a.offset[r] = base.c[C_INDEX] + cnt.c[C_INDEX];
+        } else {
+          raise_error(a.err, E_CAPACITY, x);
+        }
+        if (h.w) {
+          const uint64_t wr = base.c[C_WEIGHT] + cnt.c[C_WEIGHT];
+          if (wr < a.cap[C_WEIGHT]) a.weight[wr] = parse_float(src, h.wpos, &e, &nan_err);
+          else raise_error(a.err, E_CAPACITY, x);
+        }
+        if (nan_err) raise_error(a.err, E_NAN_LITERAL, x);
+        cnt.c[C_ROWS]++;
+        cnt.c[C_LABEL]++;
+        cnt.c[C_WEIGHT] += h.w;
       }
     }
   }
@@ -318,7 +382,8 @@ DA_HDF void tile(const LibfmArgs &a, svm::Shared &sh, BK &bk, uint64_t k) {
       sg.le = (sg.ls >> 1) | ((uint32_t)nxt << (len - 1));
     }
 
-    // ---- head sections -> R1 marks
+    // ---- head sections -> R1 marks, and the segment's row / weight counts
+    uint32_t hrow = 0, hw = 0;
     if (sg.ls) {
       uint32_t m = sg.ls;
       int chunk = sg.chunk;
@@ -333,28 +398,42 @@ DA_HDF void tile(const LibfmArgs &a, svm::Shared &sh, BK &bk, uint64_t k) {
           if (h.r1 < wend) atomic_or_u32(&sh.r1bits[(h.r1 - w0) >> 5], 1u << ((h.r1 - w0) & 31));
           else sh.pending[j & 1] = h.r1;  // only the window's last line can get here
         }
+        if (h.row) {
+          ++hrow;
+          hw += h.w;
+        }
       }
     }
     bk.sync();
 
-    // ---- transition function of my segment, then block scan
+    // ---- role masks and transition function of my segment, then block scan
     uint32_t fn = kIdentityFn;
-    Cnt dummy = zero;
-    Base64 nob;
-    for (int i = 0; i < C_N; ++i) nob.c[i] = 0;
-    if (sg.lo < sg.hi) walk<0>(a, src, sh.r1bits, w0, sg, fn, dummy, nob);
+    Roles R;
+    if (sg.lo < sg.hi) walk_roles(a, src, sh.r1bits, w0, sg, fn, R);
+    else
+      for (int s2 = 0; s2 < 4; ++s2) R.pr[s2] = R.va[s2] = R.dp[s2] = R.dv[s2] = 0, R.neg = ~0u;
     uint32_t fn_total;
     const uint32_t fn_ex = bk.exclusive(fn, kIdentityFn, FnCompose(), &fn_total);
     const uint32_t st = (fn_ex >> (2 * st0)) & 3u;
     const uint32_t st_next = (fn_total >> (2 * st0)) & 3u;
+    const uint32_t P = pick(R.pr, st), V = pick(R.va, st), DP = pick(R.dp, st), DV = pick(R.dv, st);
+    const uint32_t neg = (R.neg >> (8 * st)) & 0xFFu;
 
-    // ---- count walk, then (write pass) scan + emit walk
+    // ---- counts by popcount, then (write pass) scan + emit
     Cnt c = zero;
-    if (sg.lo < sg.hi) {
-      uint32_t s2 = st;
-      walk<1>(a, src, sh.r1bits, w0, sg, s2, c, nob, mp, dtp);
-    }
+    c.c[C_ROWS] = c.c[C_LABEL] = hrow;
+    c.c[C_WEIGHT] = hw;
+    c.c[C_INDEX] = c.c[C_FIELD] = (uint32_t)popc32(P | DP);
+    c.c[C_VALUE] = (uint32_t)popc32(V | DV);
     if (MODE == 1) {
+      if (mp && (P | DP))
+        for_pairs(a, src, sg, P, DP, dtp, [&](uint64_t, uint64_t fv, uint64_t iv, uint64_t, int chunk) {
+          if (!a.wide) {
+            fv = (uint32_t)fv;
+            iv = (uint32_t)iv;
+          }
+          mp->add(a.chunk_min, chunk, fv < iv ? fv : iv);
+        });
       mine = CntAdd()(mine, c);
     } else {
       Cnt wtot;
@@ -362,9 +441,7 @@ DA_HDF void tile(const LibfmArgs &a, svm::Shared &sh, BK &bk, uint64_t k) {
       if (sg.lo < sg.hi) {
         Base64 b;
         for (int i = 0; i < C_N; ++i) b.c[i] = tbase.c[i] + tot.c[i] + ex.c[i];
-        Cnt local = zero;
-        uint32_t s3 = st;
-        walk<2>(a, src, sh.r1bits, w0, sg, s3, local, b, nullptr, dtp);
+        emit(a, src, sg, P, V, DP, DV, neg, b, dtp);
       }
       tot = CntAdd()(tot, wtot);
     }
