@@ -42,11 +42,13 @@ struct LibsvmArgs {
   const uint32_t *gate;  // when set, the tile kernels run only if *gate != 0
   UnitLim ul;            // decoder limit per unit
   DA_HD uint64_t lim(int unit) const { return ul.lim(unit); }
-  // libsvm: what the count pass learnt per window for the write pass (NULL:
-  // the write pass works it out again): rec [ntiles][rec_win][4][kThreads]
+  // libsvm / libfm: what the count pass learnt per window for the write pass
+  // (NULL: the write pass works it out again): rec [ntiles][rec_win][4][kThreads]
   // words -- index / value / dangling-value role masks and packed head
-  // counts per thread -- and rec_meta [ntiles][rec_win][2]: the R1 carried
-  // past the window and the role state after it
+  // counts per thread (libfm: pair / value / dangling masks, head counts and
+  // the sign-error position) -- and rec_meta [ntiles][rec_win][2]: the R1
+  // carried past the window and the role state after it (libfm: bit 8 set =
+  // the window has no record)
   uint32_t *rec;
   uint64_t *rec_meta;
   uint32_t rec_win;  // windows per tile with a record (the rest: worked out again)

@@ -143,10 +143,10 @@ const char *dmlc_amd_error_string(int code) {
 int units_per_chunk(const dmlc_amd_params *p) { return p && p->nthread > 1 ? p->nthread : 1; }
 constexpr int kMaxNthread = 1 << 12;
 
-// the exact libsvm / CSV kernels' count-pass records (args.h exact_rec_*):
-// bytes, 0 when the format has none or they would outgrow the text
+// the exact kernels' count-pass records (args.h exact_rec_*): bytes, 0 when
+// they would outgrow the text
 uint64_t rec_bytes_of(uint64_t nbytes, uint64_t T, uint64_t ntiles, const dmlc_amd_params *prm) {
-  if (!prm || prm->format == DMLC_AMD_LIBFM) return 0;
+  if (!prm) return 0;
   const uint64_t b = dmlc_amd::exact_rec_bytes(ntiles, dmlc_amd::exact_rec_win(T, dmlc_amd::kWin), dmlc_amd::kThreads);
   return dmlc_amd::exact_rec_on(nbytes, b) ? b : 0;
 }

@@ -132,7 +132,7 @@ DA_HDF void walk_roles(const LibfmArgs &a, Src &src, const uint32_t *r1bits, uin
         fn = kAllA;
         amask = 0xFu;
       } else if (fn != kAllPre) {
-        const bool colon = gap_fnb(src, x, cfloor) == ':';
+        const bool colon = (sg.xg & bit) ? gap_fnb(src, x, cfloor) == ':' : (sg.rc & bit) != 0u;
         for (int s = 0; s < 4; ++s) {
           const uint32_t e = (fn >> (2 * s)) & 3u;
           if (e == S_A && colon) R.pr[s] |= bit;
@@ -322,7 +322,27 @@ DA_HDF void tile(const LibfmArgs &a, svm::Shared &sh, BK &bk, uint64_t k) {
   Src src;
   src.g = a.text;
   src.lds = sh.win;
+  // the count pass's records of this tile's windows (args.h LibsvmArgs.rec,
+  // libsvm_core.h): the write pass takes the role masks and head counts from
+  // them instead of walking the window again.  A window in which some start
+  // state leaves both a dangling pair and a dangling value in one segment
+  // (their kinds would need a fifth word) gets none: its meta word says so
+  // and the write pass walks it, from the state the meta words carry.
+  const bool recs = a.rec != nullptr;
+  uint32_t *rec_t = recs ? a.rec + (uint64_t)k * a.rec_win * 4 * kThreads : nullptr;
+  uint64_t *meta_t = recs ? a.rec_meta + (uint64_t)k * a.rec_win * 2 : nullptr;
+  constexpr uint64_t kWalkWin = 1u << 8;
+  bool prev_rec = false;  // write pass: window j-1 came from its record
   while (!done) {
+    const bool has_rec = recs && (uint32_t)j < a.rec_win;
+    const bool from_rec = MODE == 2 && has_rec && !(meta_t[j * 2 + 1] & kWalkWin);
+    if (MODE == 2 && prev_rec && !from_rec) {  // walking again after recorded windows
+      st0 = (uint32_t)(meta_t[(j - 1) * 2 + 1] & 3u);
+      if (tid == 0) sh.pending[(j + 1) & 1] = meta_t[(j - 1) * 2];
+      bk.sync();
+    }
+    prev_rec = from_rec;
+    if (MODE == 1 && tid == 0) sh.walk_win = 0;
     const uint64_t pend = sh.pending[(j + 1) & 1];  // written during window j-1
     uint64_t wend = mn(w0 + (uint64_t)kWin, a.n);
     if (wend == a.n) done = true;
@@ -357,23 +377,28 @@ DA_HDF void tile(const LibfmArgs &a, svm::Shared &sh, BK &bk, uint64_t k) {
     Seg sg;
     sg.lo = w0 + (uint64_t)tid * kSeg;
     sg.hi = mn(sg.lo + (uint64_t)kSeg, wend);
-    sg.rs = sg.ls = sg.le = 0;
+    sg.rs = sg.ls = sg.le = sg.rc = sg.rh = sg.xg = 0;
     sg.chunk = 0;
     if (sg.lo < sg.hi) {
       sg.chunk = chunk_of(a.cs, a.nchunk, sg.lo);
       src.lim = a.lim(sg.chunk);
-      uint32_t dm = 0, nl = 0, csm = 0;
+      uint32_t dm, nl, cm = 0, bm = 0, hm = 0, csm = 0;
       const int len = (int)(sg.hi - sg.lo);
-      for (int i = 0; i < len; ++i) {
-        const uint32_t c = sh.win[sg.lo + i - abase];
-        dm |= (uint32_t)is_digitchar(c) << i;
-        nl |= (uint32_t)is_nl(c) << i;
-      }
+      if (from_rec) seg_masks(sh.win, (uint32_t)(sg.lo - abase), len, &dm, &nl);
+      else seg_masks5(sh.win, (uint32_t)(sg.lo - abase), len, &dm, &nl, &cm, &bm, &hm);
       for (int c = sg.chunk; c < a.nchunk && a.cs[c] < sg.hi; ++c)
         if (a.cs[c] >= sg.lo) csm |= 1u << (a.cs[c] - sg.lo);
       const uint32_t prev = (sg.lo > 0 && !(csm & 1u) && is_digitchar(src(sg.lo - 1))) ? 1u : 0u;
       sg.rs = (dm & ~((dm << 1) | prev)) | (csm & dm);
       sg.ls = nl | csm;
+      if (!from_rec) {  // gap classes (libsvm_core.h): run starts whose gap's first non-blank is ':'
+        const uint32_t lenm = len >= 32 ? ~0u : ((1u << len) - 1u);
+        const uint32_t G = ~dm & lenm, Bg = bm & G;
+        const uint32_t F = (Bg + (G & ~(G << 1))) & ~Bg & G;
+        sg.rc = (G + (F & cm)) & ~G & dm;
+        const uint32_t rs0 = sg.rs & (0u - sg.rs);  // the first run's gap may begin before the segment
+        sg.xg = (dm & (rs0 - 1u)) == 0u ? rs0 : 0u;
+      }
       bool nxt = sg.hi == a.n;
       if (!nxt) {
         const uint64_t h = sg.hi;
@@ -384,7 +409,7 @@ DA_HDF void tile(const LibfmArgs &a, svm::Shared &sh, BK &bk, uint64_t k) {
 
     // ---- head sections -> R1 marks, and the segment's row / weight counts
     uint32_t hrow = 0, hw = 0;
-    if (sg.ls) {
+    if (sg.ls && !from_rec) {
       uint32_t m = sg.ls;
       int chunk = sg.chunk;
       while (m) {
@@ -407,17 +432,49 @@ DA_HDF void tile(const LibfmArgs &a, svm::Shared &sh, BK &bk, uint64_t k) {
     bk.sync();
 
     // ---- role masks and transition function of my segment, then block scan
-    uint32_t fn = kIdentityFn;
-    Roles R;
-    if (sg.lo < sg.hi) walk_roles(a, src, sh.r1bits, w0, sg, fn, R);
-    else
-      for (int s2 = 0; s2 < 4; ++s2) R.pr[s2] = R.va[s2] = R.dp[s2] = R.dv[s2] = 0, R.neg = ~0u;
-    uint32_t fn_total;
-    const uint32_t fn_ex = bk.exclusive(fn, kIdentityFn, FnCompose(), &fn_total);
-    const uint32_t st = (fn_ex >> (2 * st0)) & 3u;
-    const uint32_t st_next = (fn_total >> (2 * st0)) & 3u;
-    const uint32_t P = pick(R.pr, st), V = pick(R.va, st), DP = pick(R.dp, st), DV = pick(R.dv, st);
-    const uint32_t neg = (R.neg >> (8 * st)) & 0xFFu;
+    // (or the count pass's record of them)
+    uint32_t P, V, DP, DV, neg, st_next = S_PRE;
+    uint32_t *rw = has_rec ? rec_t + (uint64_t)j * 4 * kThreads : nullptr;
+    if (from_rec) {
+      P = rw[tid];
+      V = rw[kThreads + tid];
+      const uint32_t d = rw[2 * kThreads + tid], hc = rw[3 * kThreads + tid];
+      DP = (hc >> 24) & 1u ? 0u : d;  // bit 24: the dangling ends are values
+      DV = d ^ DP;
+      hrow = hc & 0x3Fu;
+      hw = (hc >> 6) & 0x3Fu;
+      neg = (hc >> 12) & 0xFFu;
+    } else {
+      uint32_t fn = kIdentityFn;
+      Roles R;
+      if (sg.lo < sg.hi) walk_roles(a, src, sh.r1bits, w0, sg, fn, R);
+      else
+        for (int s2 = 0; s2 < 4; ++s2) R.pr[s2] = R.va[s2] = R.dp[s2] = R.dv[s2] = 0, R.neg = ~0u;
+      if (MODE == 1 && rw) {
+        bool mixed = false;
+        for (int s2 = 0; s2 < 4; ++s2) mixed = mixed || (R.dp[s2] && R.dv[s2]);
+        if (mixed) sh.walk_win = 1;  // (read by thread 0 after the scan's barriers)
+      }
+      uint32_t fn_total;
+      const uint32_t fn_ex = bk.exclusive(fn, kIdentityFn, FnCompose(), &fn_total);
+      const uint32_t st = (fn_ex >> (2 * st0)) & 3u;
+      st_next = (fn_total >> (2 * st0)) & 3u;
+      P = pick(R.pr, st);
+      V = pick(R.va, st);
+      DP = pick(R.dp, st);
+      DV = pick(R.dv, st);
+      neg = (R.neg >> (8 * st)) & 0xFFu;
+      if (MODE == 1 && rw) {  // the record for the write pass
+        rw[tid] = P;
+        rw[kThreads + tid] = V;
+        rw[2 * kThreads + tid] = DP | DV;
+        rw[3 * kThreads + tid] = hrow | (hw << 6) | (neg << 12) | ((DV != 0u ? 1u : 0u) << 24);
+        if (tid == 0) {
+          meta_t[j * 2] = sh.pending[j & 1];  // (set by the heads, before the scan's barriers)
+          meta_t[j * 2 + 1] = st_next | (sh.walk_win ? kWalkWin : 0u);
+        }
+      }
+    }
 
     // ---- counts by popcount, then (write pass) scan + emit
     Cnt c = zero;

@@ -110,6 +110,7 @@ struct Shared {  // LDS of one workgroup
   uint32_t r1bits[kWin / 32 + 1];
   uint64_t pending[2];  // R1 of a line whose head crossed a window, by window parity
   fast::DecTables dt;   // the window decoders' tables (fast_common.h)
+  uint32_t walk_win;    // libfm count pass: this window gets no record (libfm_core.h)
 };
 
 

@@ -278,9 +278,9 @@ extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *c
     a.chunk_min = chunk_min.data();
     a.err = err;
     a.gate = &gate;
-    std::vector<uint32_t> rec;  // the exact libsvm kernels' count-pass records (capi.cpp)
+    std::vector<uint32_t> rec;  // the exact libsvm / libfm kernels' count-pass records (capi.cpp)
     std::vector<uint64_t> rec_meta;
-    if (!fm) {
+    if (!std::getenv("EMU_NOREC")) {  // (EMU_NOREC: records off, test_emu.py self-checks)
       const uint32_t rw = exact_rec_win(T, kWin);
       if (exact_rec_on(nbytes, exact_rec_bytes(ntiles, rw, kThreads))) {
         rec.assign(ntiles * rw * 4 * kThreads, 0xCDCDCDCDu);  // device memory is not zeroed either
@@ -317,7 +317,8 @@ extern "C" int emu_parse(const uint8_t *text, uint64_t nbytes, const uint64_t *c
       f.res = res;
       // the lean kernel first on a full call (libsvm.hip launch_libsvm)
       const char *le = std::getenv("DMLC_AMD_LEAN");
-      const bool lean = !fm && !count_only && prm->indexing_mode >= 0 && !(le && le[0] == '0');  // (on unless turned off)
+      // (off unless DMLC_AMD_LEAN=1, as in the product build: libsvm.hip LSVM_DEFAULT)
+      const bool lean = !fm && !count_only && prm->indexing_mode >= 0 && le && le[0] && le[0] != '0';
       std::vector<uint64_t> llb(nft * 5 + 1, 0);
       if (lean) {
         f.lean_lb = llb.data();

@@ -59,19 +59,26 @@ def test_workspace_and_argument_validation(lib):
     c = dmlc_amd.make_params("csv")  # (CSV keeps window count records too)
     wc = dmlc_amd.lib().dmlc_amd_workspace_bytes(1 << 30, 128, ctypes.byref(c))
     assert 0 < wc < (1 << 30) // tile * 64 + (1 << 20) + (1 << 30) * 6 // 10
-    fm = dmlc_amd.make_params("libfm")
+    fm = dmlc_amd.make_params("libfm")  # (libfm keeps the same records since round 6)
     wf = dmlc_amd.lib().dmlc_amd_workspace_bytes(1 << 30, 128, ctypes.byref(fm))
-    assert 0 < wf < (1 << 30) // tile * 64 + (1 << 20)  # (no records for libfm)
+    assert 0 < wf < (1 << 30) // tile * 64 + (1 << 20) + (1 << 30) * 6 // 10
     small = dmlc_amd.make_params("libsvm", tile_bytes=64)  # tiny exact tiles: records off
     assert dmlc_amd.lib().dmlc_amd_workspace_bytes(1 << 30, 128, ctypes.byref(small)) < (1 << 30) * 2
-    # records never exceed 5/8 of the text + 1 MiB (args.h exact_rec_on), whatever the exact tile
+    # records never exceed 5/8 of the text + 1 MiB (args.h exact_rec_on), whatever the exact tile;
+    # libsvm and libfm keep the same tables and records, libsvm the lean kernel's look-back words too
     for tb in (4096, 9000, 65536, 1 << 18, 1 << 20):
         q = dmlc_amd.make_params("libsvm", tile_bytes=tb)
+        base = dmlc_amd.make_params("libfm", tile_bytes=tb)
         for n in (1 << 16, 1 << 20, 32 << 20, 1 << 30):
-            base = dmlc_amd.make_params("libfm", tile_bytes=tb)  # the same tables without records
+            nft = (n + tile - 1) // tile
             extra = (dmlc_amd.lib().dmlc_amd_workspace_bytes(n, 128, ctypes.byref(q))
                      - dmlc_amd.lib().dmlc_amd_workspace_bytes(n, 128, ctypes.byref(base)))
-            assert extra <= n // 8 * 5 + (1 << 20) + 4096, (tb, n, extra)
+            assert extra == (nft * 5 + 1) * 8, (tb, n, extra)
+            ntiles = (n + tb - 1) // tb
+            rec = ntiles * (tb // 8192 + 3) * (256 * 16 + 16)  # args.h exact_rec_bytes
+            tables = dmlc_amd.lib().dmlc_amd_workspace_bytes(n, 128, ctypes.byref(base))
+            if rec <= n // 8 * 5 + (1 << 20):  # records on: they are part of the workspace
+                assert tables >= rec, (tb, n)
     # the CSV single pass keeps an 8-word look-back record per 16 KiB tile (args.h kCsvLbWords),
     # libfm 5 (kFastLbWords): with the exact kernels' records off (64-byte exact tiles) the
     # difference is those words alone -- round 6 sized CSV at 5 and its records ran into labsum

@@ -729,3 +729,60 @@ def test_emu_csv_exact_wide_rows_past_the_records():
         assert (o["status"] != 0) == failed, (it, o["msg"], h["error"])
         if not failed:
             assert diff(h, o) == [], (it, diff(h, o))
+
+
+def test_emu_libfm_exact_records_vs_oracle():
+    """libfm exact kernels with the count pass's window records (round 6,
+    libfm_core.h): lines ending in a dangling "f:i:" (ParseTriple decodes the
+    value at the line end) among value lines; inputs without values whose
+    lines end in a dangling "f:" (the index decoded at the line end); both
+    kinds mixed -- then windows whose 32-byte segments hold both carry no
+    record and are walked again, and the reference's offset / value CHECK
+    fails, as it must here too -- plus '-' fields (the sign error even for a
+    dropped triple); multi-window tiles at the default, 4 KiB and odd exact
+    tiles, random chunk cuts."""
+    rng = np.random.default_rng(606)
+    checked = 0
+    for it in range(18):
+        kind = it % 3  # 0: values + "f:i:" ends, 1: no values + "f:" ends, 2: both + signs
+        rows = []
+        for _ in range(int(rng.integers(300, 2500))):
+            r = rng.random()
+            lab = int(rng.integers(0, 3))
+            f, i = int(rng.integers(0, 50)), int(rng.integers(0, 900))
+            if r < 0.15 and kind != 0:
+                rows.append("%d %d:" % (lab, f))
+            elif r < 0.3 and kind != 1:
+                rows.append("%d %d:%d:" % (lab, f, i))
+            elif r < 0.31 and kind == 2:
+                rows.append("%d -3:4:5" % lab)
+            else:
+                fmt = "%d:%d" if kind == 1 else "%d:%d:%.4g"
+                trips = [(fmt % ((rng.integers(0, 50), rng.integers(0, 900)) if kind == 1 else
+                                 (rng.integers(0, 50), rng.integers(0, 900), rng.random())))
+                         for _ in range(int(rng.integers(0, 6)))]
+                if rng.random() < 0.2:
+                    trips.append("%d" % rng.integers(0, 50))
+                rows.append(" ".join(["%d" % lab] + trips))
+        data = ("\n".join(rows) + "\n").encode()
+        offs = fuzz_text.random_cuts(rng, data, 4)
+        o = po.parse_chunks(data, offs, fmt=po.LIBFM)
+        h = pyemu.parse(data, offs, "libfm", exact=True, tile_bytes=[0, 4096, 9000][(it // 3) % 3])
+        failed = check_fail(h, "libfm", offs)
+        assert (o["status"] != 0) == failed, (it, o["msg"], h["error"])
+        if kind != 2:
+            assert not failed, (it, o["msg"])
+            assert diff(h, o) == [], (it, diff(h, o))
+        else:
+            # the reference fails the block's CHECK, so its arrays cannot pin the walked
+            # windows: the same call without records (every window walked) must agree
+            os.environ["EMU_NOREC"] = "1"
+            try:
+                h2 = pyemu.parse(data, offs, "libfm", exact=True, tile_bytes=[0, 4096, 9000][(it // 3) % 3])
+            finally:
+                os.environ.pop("EMU_NOREC", None)
+            for k in ("offset", "label", "weight", "field", "index", "value", "chunk_table"):
+                assert np.array_equal(h[k], h2[k]), (it, k)
+            assert h["error"] == h2["error"], it
+        checked += not failed
+    assert checked >= 12, checked
