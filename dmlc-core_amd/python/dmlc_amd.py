@@ -67,7 +67,8 @@ def lib():
         L.dmlc_amd_error_string.argtypes = [ctypes.c_int]
         L.dmlc_amd_device_count.restype = ctypes.c_int
         L.dmlc_amd_abi_version.restype = ctypes.c_int
-        L.dmlc_amd_build_id.restype = ctypes.c_char_p
+        if hasattr(L, "dmlc_amd_build_id"):  # (A/B variant libraries built from older sources lack it)
+            L.dmlc_amd_build_id.restype = ctypes.c_char_p
         L.dmlc_amd_strtof_batch.restype = ctypes.c_int
         L.dmlc_amd_strtof_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
@@ -262,7 +263,8 @@ class DeviceParser:
 
 def build_id():
     """SHA-256 prefix of the sources the loaded library was built from."""
-    return lib().dmlc_amd_build_id().decode()
+    L = lib()
+    return L.dmlc_amd_build_id().decode() if hasattr(L, "dmlc_amd_build_id") else "unknown"
 
 
 def error_code(err):
