@@ -76,6 +76,13 @@ class TextSplitSource : public ChunkSource {
     return Fill{f.end, f.need};
   }
   void BeforeFirst() override { split_->BeforeFirst(); }
+  const std::vector<std::pair<const char *, size_t>> *Mappings() override {
+    return split_->Mapped() ? &split_->Mappings() : nullptr;
+  }
+  Fill FillPieces(size_t max_bytes, std::vector<uint64_t> *ends, std::vector<TextPiece> *pieces) override {
+    const TextSplit::Fill f = split_->FillPieces(max_bytes, ends, pieces);
+    return Fill{f.end, f.need};
+  }
 
  private:
   std::unique_ptr<TextSplit> split_;

@@ -57,6 +57,7 @@
 #include "dmlc/io.h"
 #include "dmlc/logging.h"
 #include "dmlc_amd.h"
+#include "text_split.h"
 
 namespace dmlc_amd {
 
@@ -170,6 +171,11 @@ class ChunkSource {
   // the next chunk might not fit; each chunk's end offset goes to *ends.
   virtual Fill FillChunks(char *dst, size_t cap, size_t max_bytes, std::vector<uint64_t> *ends) = 0;
   virtual void BeforeFirst() = 0;
+  // Sources over mapped files (TextSplit::FillPieces): the chunks as pieces of
+  // the mappings instead of a copy, and the mappings for HIP to register.
+  // Default: no such form.
+  virtual const std::vector<std::pair<const char *, size_t>> *Mappings() { return nullptr; }
+  virtual Fill FillPieces(size_t, std::vector<uint64_t> *, std::vector<TextPiece> *) { return Fill{true, 0}; }
 };
 
 // Any dmlc::InputSplit (one copy per chunk out of the split's buffer).
@@ -416,6 +422,8 @@ template <typename I, typename D>
 struct Batch {
   uint64_t seq = 0;
   PinnedVec<char> text;
+  std::vector<TextPiece> pieces;  // the text as pieces of registered mappings (text unused)
+  std::vector<std::pair<size_t, size_t>> segs;  // (mapping, segment) the pieces lie in
   PinnedVec<uint64_t> starts;  // nchunks + 1
   size_t nchunks = 0, bytes = 0;
   bool end = false;
@@ -438,6 +446,14 @@ struct Batch {
     fail_at = fail_unit = SIZE_MAX;
     error.clear();
   }
+};
+
+// A registered segment of a mapped input file (HipTextParser::PrepPieces).
+struct MapSeg {
+  const char *p = nullptr;
+  size_t len = 0;
+  bool reg = false;
+  uint64_t last_seq = 0;  // the last batch that used it (unregistered when that one is released)
 };
 
 struct EngineConfig {
@@ -519,6 +535,7 @@ class HipTextParser : public dmlc::Parser<IndexType, DType> {
     const int depth = cfg_.depth > 0 ? cfg_.depth : 2 * nworkers;
     for (int i = 0; i < nworkers + depth + 1; ++i) pool_.emplace_back(new B());
     for (int i = 0; i < nworkers; ++i) workers_.emplace_back(new Worker(cfg_.devices[i % cfg_.devices.size()]));
+    RegisterMappings();
     Start();
   }
   ~HipTextParser() override {
@@ -528,6 +545,7 @@ class HipTextParser : public dmlc::Parser<IndexType, DType> {
     if (cfg_.stats) PrintStats();
     workers_.clear();  // streams and HBM blocks back to DevCache, pinned blocks to PinnedCache
     pool_.clear();
+    UnregisterAll();
     if (cfg_.stats) {
       std::fprintf(stderr, "{\"dmlc_amd_teardown\": {\"stop_s\": %.4f, \"free_s\": %.4f}}\n", stop_ns * 1e-9,
                    (clk.ns() - stop_ns) * 1e-9);
@@ -639,6 +657,10 @@ class HipTextParser : public dmlc::Parser<IndexType, DType> {
   enum { S_READ, S_H2D, S_PARSE, S_D2H, S_BUILD, S_WAIT, S_N };
   std::atomic<uint64_t> stat_ns_[S_N] = {};
   std::atomic<uint64_t> stat_batches_{0};
+  bool pieces_ = false;  // batches as pieces of registered mappings (RegisterMappings)
+  std::vector<std::pair<const char *, size_t>> maps_;
+  std::vector<std::vector<MapSeg>> segs_;  // per mapping, its 64 MiB segments
+  std::mutex seg_mu_;
   struct Clock {
     std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
     uint64_t ns() const {
@@ -658,6 +680,112 @@ class HipTextParser : public dmlc::Parser<IndexType, DType> {
     std::fprintf(stderr, "%s}}\n", line.c_str());
   }
 
+  // Text from the page cache by DMA (round 6): when the source
+  // maps its files, each batch's text goes to HBM as hipMemcpyAsync pieces of
+  // the mappings -- no pread into a pinned block, so a host byte of text is
+  // read once (by the DMA) instead of read, written and read again.  The
+  // mappings are registered with HIP (read-only, portable) in 64 MiB
+  // segments as the reader reaches them, and a segment is unregistered when
+  // the last batch that used it is released, so the pinned part of the page
+  // cache follows the pipeline instead of the whole input.  A batch whose
+  // segment cannot be registered is staged through its pinned block
+  // (memcpy) instead; DMLC_AMD_MMAP=0 keeps the pinned-copy form throughout.
+  size_t seg_bytes_ = size_t(64) << 20;        // DMLC_AMD_MMAP_SEG_MB (A/B)
+  unsigned reg_flags_ = hipHostRegisterReadOnly;  // + Portable when batches go to several devices
+  void RegisterMappings() {
+    const auto *maps = src_->Mappings();
+    if (!maps || maps->empty()) return;
+    const char *e = std::getenv("DMLC_AMD_MMAP");
+    if (!e || e[0] != '1') return;  // opt-in (registration costs more than the copy it saves at 1 GPU)
+    if (const char *sm = std::getenv("DMLC_AMD_MMAP_SEG_MB")) seg_bytes_ = (size_t)std::max(1, std::atoi(sm)) << 20;
+    if (cfg_.devices.size() > 1 || (std::getenv("DMLC_AMD_MMAP_PORTABLE") && std::getenv("DMLC_AMD_MMAP_PORTABLE")[0] == '1'))
+      reg_flags_ |= hipHostRegisterPortable;
+    for (const auto &m : *maps) {
+      maps_.push_back(m);
+      std::vector<MapSeg> sv((m.second + seg_bytes_ - 1) / seg_bytes_);
+      for (size_t i = 0; i < sv.size(); ++i) {
+        sv[i].p = m.first + i * seg_bytes_;
+        sv[i].len = std::min(seg_bytes_, m.second - i * seg_bytes_);
+      }
+      segs_.push_back(std::move(sv));
+    }
+    pieces_ = true;
+  }
+  size_t MapOf(const char *p) const {
+    for (size_t i = 0; i < maps_.size(); ++i)
+      if (p >= maps_[i].first && p < maps_[i].first + maps_[i].second) return i;
+    throw dmlc::Error("dmlc_amd: a text piece outside the split's mappings");
+  }
+  // Reader: split the batch's pieces at segment boundaries (one registered
+  // range per copy) and register the segments it reaches; false: a
+  // registration failed (the caller stages the batch instead).
+  bool PrepPieces(B *b, uint64_t seq) {
+    std::vector<TextPiece> out;
+    b->segs.clear();
+    for (const TextPiece &pc : b->pieces) {
+      if (!pc.src) {
+        out.push_back(pc);
+        continue;
+      }
+      const size_t m = MapOf(pc.src);
+      const char *base = maps_[m].first;
+      uint64_t o = (uint64_t)(pc.src - base), dst = pc.off;
+      const uint64_t e = o + pc.len;
+      while (o < e) {
+        const uint64_t sg = o / seg_bytes_, se = std::min<uint64_t>(e, (sg + 1) * seg_bytes_);
+        out.push_back(TextPiece{dst, base + o, se - o});
+        dst += se - o;
+        if (b->segs.empty() || b->segs.back() != std::make_pair(m, (size_t)sg)) b->segs.emplace_back(m, (size_t)sg);
+        o = se;
+      }
+    }
+    b->pieces.swap(out);
+    std::lock_guard<std::mutex> lk(seg_mu_);
+    for (const auto &ms : b->segs) {
+      MapSeg &g = segs_[ms.first][ms.second];
+      if (!g.reg) {
+        if (hipHostRegister(const_cast<char *>(g.p), g.len, reg_flags_) !=
+            hipSuccess) {
+          (void)hipGetLastError();
+          return false;
+        }
+        g.reg = true;
+      }
+      g.last_seq = seq;
+    }
+    return true;
+  }
+  // the batch's text gathered into its pinned block (a segment that could not be registered)
+  void StagePieces(B *b) {
+    b->text.reserve(b->bytes + 1);
+    for (const TextPiece &pc : b->pieces) {
+      if (pc.src) std::memcpy(b->text.p + pc.off, pc.src, pc.len);
+      else b->text.p[pc.off] = '\n';
+    }
+    b->pieces.clear();
+  }
+  void ReleaseSegs(B *b) {
+    if (b->segs.empty()) return;
+    std::lock_guard<std::mutex> lk(seg_mu_);
+    for (const auto &ms : b->segs) {
+      MapSeg &g = segs_[ms.first][ms.second];
+      if (g.reg && g.last_seq == b->seq) {
+        (void)hipHostUnregister(const_cast<char *>(g.p));
+        g.reg = false;
+      }
+    }
+    b->segs.clear();
+  }
+  void UnregisterAll() {
+    std::lock_guard<std::mutex> lk(seg_mu_);
+    for (auto &sv : segs_)
+      for (MapSeg &g : sv)
+        if (g.reg) {
+          (void)hipHostUnregister(const_cast<char *>(g.p));
+          g.reg = false;
+        }
+  }
+
   void ReadLoop() {
     try {
       std::vector<uint64_t> ends;
@@ -674,13 +802,18 @@ class HipTextParser : public dmlc::Parser<IndexType, DType> {
         const Clock clk;
         // room for one more whole chunk past the target (8 MiB InputSplit buffers)
         size_t cap = cfg_.batch_bytes + (16u << 20);
-        b->text.reserve(cap);
+        if (!pieces_) b->text.reserve(cap);
         ends.clear();
         ChunkSource::Fill f;
-        for (;;) {
-          f = src_->FillChunks(b->text.p, b->text.cap, cfg_.batch_bytes, &ends);
-          if (f.need == 0) break;
-          b->text.reserve(f.need + (16u << 20));  // a record longer than the room: grow, retry
+        b->pieces.clear();
+        if (pieces_) {
+          f = src_->FillPieces(cfg_.batch_bytes, &ends, &b->pieces);
+        } else {
+          for (;;) {
+            f = src_->FillChunks(b->text.p, b->text.cap, cfg_.batch_bytes, &ends);
+            if (f.need == 0) break;
+            b->text.reserve(f.need + (16u << 20));  // a record longer than the room: grow, retry
+          }
         }
         b->nchunks = ends.size();
         b->starts.reserve(ends.size() + 1);
@@ -688,6 +821,14 @@ class HipTextParser : public dmlc::Parser<IndexType, DType> {
         for (size_t i = 0; i < ends.size(); ++i) b->starts.p[i + 1] = ends[i];
         b->bytes = ends.empty() ? 0 : ends.back();
         b->end = f.end;
+        if (!b->pieces.empty()) {  // (only the reader advances next_read_)
+          uint64_t seq;
+          {
+            std::lock_guard<std::mutex> lk(mu_);
+            seq = next_read_;
+          }
+          if (!PrepPieces(b, seq)) StagePieces(b);
+        }
         if (cfg_.stats) stat_ns_[S_READ] += clk.ns();
         {
           std::lock_guard<std::mutex> lk(mu_);
@@ -752,6 +893,7 @@ class HipTextParser : public dmlc::Parser<IndexType, DType> {
     return b;
   }
   void Release(B *b) {
+    ReleaseSegs(b);  // (in sequence order: Take hands batches out in order)
     {
       std::lock_guard<std::mutex> lk(mu_);
       free_.push_back(b);
@@ -776,7 +918,15 @@ class HipTextParser : public dmlc::Parser<IndexType, DType> {
     if (st && !w->ev[0])
       for (auto &e : w->ev) hip_check(hipEventCreate(&e), "hipEventCreate");
     if (st) hip_check(hipEventRecord(w->ev[0], s), "hipEventRecord");
-    H2D(d_text, b->text.p, b->bytes, s);
+    if (!b->pieces.empty()) {  // DMA straight from the registered mappings; inserted '\n's by memset
+      for (const TextPiece &pc : b->pieces) {
+        char *dst = static_cast<char *>(d_text) + pc.off;
+        if (pc.src) hip_check(hipMemcpyAsync(dst, pc.src, pc.len, hipMemcpyHostToDevice, s), "H2D piece");
+        else hip_check(hipMemsetAsync(dst, '\n', 1, s), "H2D newline");
+      }
+    } else {
+      H2D(d_text, b->text.p, b->bytes, s);
+    }
     hip_check(hipMemcpyAsync(d_cs, b->starts.p, (nch + 1) * 8, hipMemcpyHostToDevice, s), "H2D chunk starts");
     if (st) hip_check(hipEventRecord(w->ev[1], s), "hipEventRecord");
     dmlc_amd_params p = cfg_.prm;

@@ -190,4 +190,47 @@ extern "C" int dmlc_amd_host_split_inplace(const char *uri, unsigned part, unsig
   }
 }
 
+// Test hook: the same chunk sequence through TextSplit::FillPieces (the
+// mapped form: pieces of the files' mappings, DMA'd by the device pipeline),
+// the bytes gathered from the pieces.  Fails (DMLC_AMD_ERR_ARG) when the
+// split did not map its files.
+extern "C" int dmlc_amd_host_split_pieces(const char *uri, unsigned part, unsigned nparts, uint64_t buffer_bytes,
+                                          uint64_t batch_bytes, char **out_buf, uint64_t **out_off,
+                                          uint64_t *out_n) {
+  try {
+    dmlc_amd::TextSplit split(uri, part, nparts, buffer_bytes);
+    if (!split.Mapped()) return DMLC_AMD_ERR_ARG;
+    std::vector<char> all;
+    std::vector<uint64_t> off(1, 0), ends;
+    std::vector<dmlc_amd::TextPiece> pv;
+    for (;;) {
+      ends.clear();
+      const dmlc_amd::TextSplit::Fill f = split.FillPieces(batch_bytes, &ends, &pv);
+      std::vector<char> batch;
+      for (const dmlc_amd::TextPiece &pc : pv) {
+        if (pc.off != batch.size()) return DMLC_AMD_ERR_ARG;  // pieces must tile the batch
+        if (pc.src) batch.insert(batch.end(), pc.src, pc.src + pc.len);
+        else batch.push_back('\n');
+      }
+      uint64_t prev = 0;
+      for (uint64_t e : ends) {
+        if (e > batch.size()) return DMLC_AMD_ERR_ARG;
+        all.insert(all.end(), batch.data() + prev, batch.data() + e);
+        off.push_back(all.size());
+        prev = e;
+      }
+      if (prev != batch.size()) return DMLC_AMD_ERR_ARG;  // the batch is its chunks
+      if (f.end) break;
+    }
+    *out_buf = static_cast<char *>(std::malloc(all.size() + 1));
+    std::memcpy(*out_buf, all.data(), all.size());
+    *out_off = static_cast<uint64_t *>(std::malloc(off.size() * 8));
+    std::memcpy(*out_off, off.data(), off.size() * 8);
+    *out_n = off.size() - 1;
+    return 0;
+  } catch (const std::exception &) {
+    return DMLC_AMD_ERR_ARG;
+  }
+}
+
 extern "C" void dmlc_amd_host_free(void *p) { std::free(p); }

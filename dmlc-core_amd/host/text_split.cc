@@ -3,6 +3,7 @@
 
 #include <dirent.h>
 #include <fcntl.h>
+#include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -157,6 +158,25 @@ TextSplit::TextSplit(const std::string &uri, unsigned part, unsigned nparts, siz
     files_.push_back(f);
     offset_.push_back(offset_.back() + sz);
   }
+  // the mapped form (FillPieces): every file read-only mapped, unless
+  // DMLC_AMD_MMAP=0 or a file cannot be (then every read is a pread)
+  const char *mm = std::getenv("DMLC_AMD_MMAP");
+  mapped_ = !(mm && mm[0] == '0') && !files_.empty();
+  for (size_t i = 0; mapped_ && i < files_.size(); ++i) {
+    const size_t sz = (size_t)(offset_[i + 1] - offset_[i]);
+    const int fd = open(files_[i].c_str(), O_RDONLY);
+    void *m = fd >= 0 ? mmap(nullptr, sz, PROT_READ, MAP_SHARED, fd, 0) : MAP_FAILED;
+    if (fd >= 0) close(fd);
+    if (m == MAP_FAILED) {
+      mapped_ = false;
+      break;
+    }
+    maps_.emplace_back((const char *)m, sz);
+  }
+  if (!mapped_) {
+    for (auto &m : maps_) munmap(const_cast<char *>(m.first), m.second);
+    maps_.clear();
+  }
   const uint64_t total = offset_.back();
   const uint64_t step = (total + nparts - 1) / nparts;
   offset_begin_ = std::min(step * part, total);
@@ -173,6 +193,7 @@ TextSplit::TextSplit(const std::string &uri, unsigned part, unsigned nparts, siz
 
 TextSplit::~TextSplit() {
   if (fd_ >= 0) close(fd_);
+  for (auto &m : maps_) munmap(const_cast<char *>(m.first), m.second);
 }
 
 size_t TextSplit::FileOf(uint64_t off) const {
@@ -316,6 +337,7 @@ uint64_t TextSplit::SeekRecordBegin(size_t file, uint64_t pos) {
 
 void TextSplit::BeforeFirst() {
   overflow_.clear();
+  overflow_pieces_.clear();
   offset_curr_ = offset_begin_;
   if (offset_begin_ >= offset_end_ || files_.empty()) return;
   file_ptr_ = FileOf(offset_begin_);
@@ -428,6 +450,118 @@ TextSplit::Fill TextSplit::FillChunks(char *dst, size_t cap, size_t max_bytes, s
     if (!cut_made) break;
   }
   overflow_.assign(dst + pos, dst + pos + olen);
+  return f;
+}
+
+// Read's walk over the files as pieces of their mappings (no copy): up to
+// `want` bytes of the part appended to *pv at offset *size.
+size_t TextSplit::ReadPieces(std::vector<TextPiece> *pv, uint64_t *size, size_t want) {
+  if (offset_begin_ >= offset_end_) return 0;
+  if (offset_curr_ + want > offset_end_) want = offset_end_ - offset_curr_;
+  if (want == 0) return 0;
+  size_t left = want;
+  while (fd_ >= 0) {
+    const uint64_t remain = offset_[file_ptr_ + 1] - offset_[file_ptr_] - file_pos_;
+    const size_t n = (size_t)std::min<uint64_t>(left, remain);
+    if (n) {
+      const char *src = maps_[file_ptr_].first + file_pos_;
+      if (!pv->empty() && pv->back().src && pv->back().src + pv->back().len == src) pv->back().len += n;
+      else pv->push_back(TextPiece{*size, src, n});
+      *size += n;
+    }
+    left -= n;
+    file_pos_ += n;
+    offset_curr_ += n;
+    if (left == 0) break;
+    pv->push_back(TextPiece{*size, nullptr, 1});  // end of this file: newline, then the next file
+    *size += 1;
+    --left;
+    if (file_ptr_ + 1 >= files_.size()) break;
+    OpenAt(++file_ptr_, 0);
+  }
+  return want - left;
+}
+
+namespace {
+// the last '\n' / '\r' in batch bytes [lo, hi) of the pieces (hi if none)
+uint64_t last_newline(const std::vector<TextPiece> &pv, uint64_t lo, uint64_t hi) {
+  for (size_t i = pv.size(); i-- > 0;) {
+    const TextPiece &p = pv[i];
+    if (p.off >= hi) continue;
+    if (p.off + p.len <= lo) break;
+    const uint64_t a = std::max(p.off, lo), b = std::min(p.off + p.len, hi);
+    if (!p.src) return a;  // an inserted newline (one byte)
+    for (uint64_t x = b; x-- > a;) {
+      const char c = p.src[x - p.off];
+      if (c == '\n' || c == '\r') return x;
+    }
+  }
+  return hi;
+}
+}  // namespace
+
+// FillChunks over the mapped files: the same reads, cuts and carried
+// remainder, with the bytes left where they are (pieces of the mappings).
+TextSplit::Fill TextSplit::FillPieces(size_t max_bytes, std::vector<uint64_t> *ends, std::vector<TextPiece> *pv) {
+  pv->clear();
+  uint64_t size = 0;
+  for (const TextPiece &p : overflow_pieces_) {
+    pv->push_back(TextPiece{size, p.src, p.len});
+    size += p.len;
+  }
+  size_t olen = (size_t)size;
+  size_t pos = 0;
+  Fill f{false, 0};
+  while (pos < max_bytes) {
+    size_t words = buffer_bytes_ / 4 + 1;  // as NextChunk: B, 2B+4, 4B+12, ...
+    bool cut_made = false;
+    for (;;) {
+      const size_t C = (words - 1) * 4;
+      if (C <= olen) {
+        words *= 2;
+        continue;
+      }
+      size_t n = ReadPieces(pv, &size, C - olen) + olen;
+      if (n == 0) {
+        f.end = true;
+        break;
+      }
+      if (n == olen) {  // end of input mid-record
+        pv->push_back(TextPiece{size, nullptr, 1});
+        size += 1;
+        ++n;
+      }
+      // cut after the last newline at chunk offset >= 1
+      const uint64_t nl = last_newline(*pv, pos + 1, pos + n);
+      if (nl == pos + n) {  // no record boundary yet: read on with a bigger buffer
+        olen = n;
+        words *= 2;
+        continue;
+      }
+      const size_t cut = (size_t)(nl - pos) + 1;
+      pos += cut;
+      olen = n - cut;
+      ends->push_back(pos);
+      cut_made = true;
+      break;
+    }
+    if (!cut_made) break;
+  }
+  // the remainder [pos, size) is carried as pieces; the batch keeps [0, pos)
+  overflow_pieces_.clear();
+  std::vector<TextPiece> keep;
+  for (const TextPiece &p : *pv) {
+    if (p.off < pos) {
+      TextPiece q = p;
+      if (q.off + q.len > pos) q.len = pos - q.off;
+      keep.push_back(q);
+    }
+    if (p.off + p.len > pos) {
+      const uint64_t a = std::max<uint64_t>(p.off, pos);
+      overflow_pieces_.push_back(TextPiece{0, p.src ? p.src + (a - p.off) : nullptr, p.off + p.len - a});
+    }
+  }
+  pv->swap(keep);
   return f;
 }
 

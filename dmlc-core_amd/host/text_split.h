@@ -22,9 +22,19 @@
 #include <cstdint>
 #include <cstdio>
 #include <string>
+#include <utility>
 #include <vector>
 
 namespace dmlc_amd {
+
+// A piece of a batch's text without a host copy (TextSplit::FillPieces): len
+// bytes at src -- inside a file mapped by the split -- for batch offset off;
+// src == nullptr: one inserted '\n'.
+struct TextPiece {
+  uint64_t off;
+  const char *src;
+  uint64_t len;
+};
 
 class TextSplit {
  public:
@@ -46,6 +56,15 @@ class TextSplit {
     size_t need;  // > 0: not even one chunk fits; call again with cap >= need
   };
   Fill FillChunks(char *dst, size_t cap, size_t max_bytes, std::vector<uint64_t> *ends);
+  // The same chunks as pieces of the mapped files (no host copy): the batch's
+  // text is the pieces in order, its chunk ends go to *ends as above, until
+  // at least max_bytes are described.  Only when Mapped(); the two forms must
+  // not be mixed between BeforeFirst calls.
+  Fill FillPieces(size_t max_bytes, std::vector<uint64_t> *ends, std::vector<TextPiece> *pieces);
+  // Every file mapped read-only (DMLC_AMD_MMAP unset or not "0", every file
+  // regular and mappable): the mappings, for the caller to register with HIP.
+  bool Mapped() const { return mapped_; }
+  const std::vector<std::pair<const char *, size_t>> &Mappings() const { return maps_; }
   // Rewind to the start of the part.
   void BeforeFirst();
   // Bytes of this part's byte range consumed so far.
@@ -68,6 +87,11 @@ class TextSplit {
   uint64_t file_pos_ = 0;  // read position in files_[file_ptr_]
   size_t buffer_bytes_;
   std::vector<char> overflow_;  // partial record carried to the next chunk
+  // mapped form: every file's mapping, and the carried partial record as pieces
+  size_t ReadPieces(std::vector<TextPiece> *pv, uint64_t *size, size_t want);
+  bool mapped_ = false;
+  std::vector<std::pair<const char *, size_t>> maps_;
+  std::vector<TextPiece> overflow_pieces_;
 };
 
 // Expand a URI path (file, directory or ';'-separated list) into file paths.

@@ -36,7 +36,24 @@ def _host():
     L.dmlc_amd_host_split_inplace.argtypes = [ctypes.c_char_p, ctypes.c_uint, ctypes.c_uint, ctypes.c_uint64,
                                               ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p),
                                               ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint64)]
+    L.dmlc_amd_host_split_pieces.argtypes = [ctypes.c_char_p, ctypes.c_uint, ctypes.c_uint, ctypes.c_uint64,
+                                             ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p),
+                                             ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint64)]
     return L
+
+
+def host_split_pieces(uri, part, nparts, buffer_bytes, batch_bytes):
+    """The chunks through TextSplit::FillPieces (pieces of the mapped files, the
+    device pipeline's DMA form since round 6), gathered back into bytes."""
+    L = _host()
+    buf, off, n = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_uint64()
+    assert L.dmlc_amd_host_split_pieces(uri.encode(), part, nparts, buffer_bytes, batch_bytes,
+                                        ctypes.byref(buf), ctypes.byref(off), ctypes.byref(n)) == 0
+    offs = np.ctypeslib.as_array(ctypes.cast(off, ctypes.POINTER(ctypes.c_uint64)), (n.value + 1,)).copy()
+    data = ctypes.string_at(buf, int(offs[-1])) if offs[-1] else b""
+    L.dmlc_amd_host_free(buf)
+    L.dmlc_amd_host_free(off)
+    return [data[int(a):int(b)] for a, b in zip(offs[:-1], offs[1:])]
 
 
 def host_split(uri, part, nparts, buffer_bytes):
@@ -108,6 +125,8 @@ def test_host_split_matches_oracle(tmp_path):
             batch = int(rng.choice([1, 3 * buf, 1 << 20]))
             cap = int(rng.choice([buf + 1, 2 * buf + 7, 4 << 20, 40 << 20]))
             assert host_split_inplace(uri, part, nparts, buf, batch, cap) == exp, (it, part, nparts, buf, batch, cap)
+            # the mapped form: the same chunks as pieces of the files' mappings
+            assert host_split_pieces(uri, part, nparts, buf, batch) == exp, (it, part, nparts, buf, batch)
         for p in paths:
             os.remove(p)
 
@@ -125,6 +144,7 @@ def test_host_split_golden_chunking(case, tmp_path):
     got = host_split(";".join(paths), case["part"], case["nparts"], 8 << 20)
     assert [len(c) for c in got] == case["chunk_sizes"]
     assert [hashlib.sha256(c).hexdigest() for c in got] == case["chunk_sha256"]
+    assert host_split_pieces(";".join(paths), case["part"], case["nparts"], 8 << 20, 32 << 20) == got
 
 
 def _host_split_error(uri):
@@ -255,15 +275,20 @@ def test_api_unittest_inputsplit_scenarios(tmp_path):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("mmap", ["0", "1"])
 @pytest.mark.parametrize("fmt", ["libsvm", "csv"])
-def test_api_synthetic_multifile_multipart(tmp_path, fmt):
+def test_api_synthetic_multifile_multipart(tmp_path, fmt, mmap):
+    """Multi-file, multi-part inputs; mmap=1: the text DMA'd from the files'
+    registered mappings (TextSplit::FillPieces, 1 MiB segments: pieces split at
+    segment ends, segments unregistered as their last batch is released)."""
     rng = np.random.default_rng(11 if fmt == "libsvm" else 12)
     f = synth.LIBSVM if fmt == "libsvm" else synth.CSV
     contents = _random_files(rng, f, 4)
     d, _ = _write(tmp_path / fmt, contents)
+    env = {"DMLC_AMD_MMAP": mmap, "DMLC_AMD_MMAP_SEG_MB": "1"}
     for nparts in (1, 3):
         for part in range(nparts):
-            h = run_api(tmp_path, d, part, nparts, fmt)
+            h = run_api(tmp_path, d, part, nparts, fmt, env=env)
             o, nch = oracle_files(contents, part, nparts, fmt=po.LIBSVM if fmt == "libsvm" else po.CSV, d=d)
             assert "error" not in h, (h, part, nparts, [len(c) for c in contents])
             assert diff(h, o) == [], (part, nparts)
@@ -291,11 +316,15 @@ def test_api_libfm_parser_and_rowiter(tmp_path):
 
 
 @pytest.mark.gpu
-def test_api_large_multibatch_and_rowiter(tmp_path, monkeypatch):
-    """Several 8 MiB chunks and several device batches; RowBlockIter concat + NumCol."""
+@pytest.mark.parametrize("mmap", ["0", "1"])
+def test_api_large_multibatch_and_rowiter(tmp_path, monkeypatch, mmap):
+    """Several 8 MiB chunks and several device batches; RowBlockIter concat + NumCol
+    (mmap=1: the text from the registered mappings in 1 MiB segments)."""
     text, _ = synth.rows(synth.LIBSVM, 60000, 128, seed=4)
     d, _ = _write(tmp_path / "big", [text.tobytes()])
     monkeypatch.setenv("DMLC_AMD_BATCH_BYTES", str(24 << 20))
+    monkeypatch.setenv("DMLC_AMD_MMAP", mmap)
+    monkeypatch.setenv("DMLC_AMD_MMAP_SEG_MB", "1")
     h = run_api(tmp_path, d)
     o, nch = oracle_files([text.tobytes()])
     assert diff(h, o) == []
