@@ -658,6 +658,7 @@ class HipTextParser : public dmlc::Parser<IndexType, DType> {
   std::atomic<uint64_t> stat_ns_[S_N] = {};
   std::atomic<uint64_t> stat_batches_{0};
   bool pieces_ = false;  // batches as pieces of registered mappings (RegisterMappings)
+  bool keep_ = false;    // registrations kept until the parser ends (RegisterMappings)
   std::vector<std::pair<const char *, size_t>> maps_;
   std::vector<std::vector<MapSeg>> segs_;  // per mapping, its 64 MiB segments
   std::mutex seg_mu_;
@@ -700,6 +701,16 @@ class HipTextParser : public dmlc::Parser<IndexType, DType> {
     if (const char *sm = std::getenv("DMLC_AMD_MMAP_SEG_MB")) seg_bytes_ = (size_t)std::max(1, std::atoi(sm)) << 20;
     if (cfg_.devices.size() > 1 || (std::getenv("DMLC_AMD_MMAP_PORTABLE") && std::getenv("DMLC_AMD_MMAP_PORTABLE")[0] == '1'))
       reg_flags_ |= hipHostRegisterPortable;
+    // segments stay registered across epochs (BeforeFirst re-reads the same
+    // pages) while the input fits DMLC_AMD_MMAP_KEEP_MB (default: an eighth of
+    // host memory, at most 64 GiB); past it each is unregistered when its
+    // last batch is released
+    size_t total = 0;
+    for (const auto &m : *maps) total += m.second;
+    size_t keep = std::min<size_t>((size_t)sysconf(_SC_PHYS_PAGES) * (size_t)sysconf(_SC_PAGESIZE) / 8,
+                                   size_t(64) << 30);
+    if (const char *k = std::getenv("DMLC_AMD_MMAP_KEEP_MB")) keep = (size_t)std::strtoull(k, nullptr, 10) << 20;
+    keep_ = total <= keep;
     for (const auto &m : *maps) {
       maps_.push_back(m);
       std::vector<MapSeg> sv((m.second + seg_bytes_ - 1) / seg_bytes_);
@@ -766,6 +777,10 @@ class HipTextParser : public dmlc::Parser<IndexType, DType> {
   }
   void ReleaseSegs(B *b) {
     if (b->segs.empty()) return;
+    if (keep_) {  // kept for the next epoch; UnregisterAll at the end
+      b->segs.clear();
+      return;
+    }
     std::lock_guard<std::mutex> lk(seg_mu_);
     for (const auto &ms : b->segs) {
       MapSeg &g = segs_[ms.first][ms.second];

@@ -319,12 +319,15 @@ def test_api_libfm_parser_and_rowiter(tmp_path):
 @pytest.mark.parametrize("mmap", ["0", "1"])
 def test_api_large_multibatch_and_rowiter(tmp_path, monkeypatch, mmap):
     """Several 8 MiB chunks and several device batches; RowBlockIter concat + NumCol
-    (mmap=1: the text from the registered mappings in 1 MiB segments)."""
+    (mmap=1: the text from the registered mappings in 1 MiB segments, each
+    unregistered when its last batch is released; the multi-file test keeps
+    them for the parser's life)."""
     text, _ = synth.rows(synth.LIBSVM, 60000, 128, seed=4)
     d, _ = _write(tmp_path / "big", [text.tobytes()])
     monkeypatch.setenv("DMLC_AMD_BATCH_BYTES", str(24 << 20))
     monkeypatch.setenv("DMLC_AMD_MMAP", mmap)
     monkeypatch.setenv("DMLC_AMD_MMAP_SEG_MB", "1")
+    monkeypatch.setenv("DMLC_AMD_MMAP_KEEP_MB", "0")  # segments unregistered as their last batch is released
     h = run_api(tmp_path, d)
     o, nch = oracle_files([text.tobytes()])
     assert diff(h, o) == []
