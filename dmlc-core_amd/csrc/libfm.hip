@@ -15,7 +15,7 @@ namespace {
 
 template <int MODE>
 #ifndef FEX_MINW
-#define FEX_MINW 4  // waves per SIMD the exact tile kernels are register-budgeted for (round 4: 1 -> 4, libfm 1M x 64 exact 22.4 -> 19.7 ms)
+#define FEX_MINW 5  // waves per SIMD the exact tile kernels are register-budgeted for (round 4: 1 -> 4, libfm 1M x 64 exact 22.4 -> 19.7 ms; round 6, with the role masks and records: 4 / 5 / 6 -> 7.15 / 6.74 / 7.76 ms, profiles/r6_ab/ab_exact_minw.txt)
 #endif
 __global__ void __launch_bounds__(kThreads, FEX_MINW) libfm_tile(LibfmArgs a) {
   __shared__ __attribute__((aligned(16))) svm::Shared sh;
