@@ -2,6 +2,7 @@
 #include "text_split.h"
 
 #include <dirent.h>
+#include <sched.h>
 #include <fcntl.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
@@ -10,6 +11,7 @@
 #include <cerrno>
 #include <algorithm>
 #include <condition_variable>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <functional>
@@ -212,6 +214,25 @@ bool TextSplit::OpenAt(size_t file, uint64_t pos) {
   return true;
 }
 
+// CPUs this process may use: its affinity mask, capped by a cgroup v2 CPU
+// quota (cpu.max "quota period"; a GPU box's job gets a share of a large
+// machine, whose processor count hardware_concurrency reports).
+unsigned cpu_share() {
+  unsigned n = std::max(1u, std::thread::hardware_concurrency());
+  cpu_set_t set;
+  if (sched_getaffinity(0, sizeof(set), &set) == 0) n = std::min<unsigned>(n, std::max(1, (int)CPU_COUNT(&set)));
+  if (FILE *f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
+    char q[32] = {0};
+    unsigned long long period = 0;
+    if (std::fscanf(f, "%31s %llu", q, &period) == 2 && std::strcmp(q, "max") != 0 && period > 0) {
+      const unsigned long long quota = std::strtoull(q, nullptr, 10);
+      n = std::min<unsigned>(n, (unsigned)std::max<unsigned long long>(1, (quota + period - 1) / period));
+    }
+    std::fclose(f);
+  }
+  return n;
+}
+
 // Process-wide pool of reader threads (started once, never joined: no thread
 // work at process exit).  ReadAt hands each a piece of a chunk; spawning and
 // joining threads per 8 MiB chunk cost a fifth of the read time.
@@ -252,8 +273,7 @@ class ReadPool {
  private:
   ReadPool() {
     const char *e = std::getenv("DMLC_AMD_READ_THREADS");
-    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-    nthreads_ = (size_t)std::min<unsigned>(e ? std::max(1, std::atoi(e)) : 8u, hw);
+    nthreads_ = (size_t)std::min<unsigned>(e ? std::max(1, std::atoi(e)) : 8u, cpu_share());
     for (size_t i = 1; i < nthreads_; ++i) std::thread([this] { loop(); }).detach();
   }
   void loop() {
